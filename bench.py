@@ -1,0 +1,164 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Msamples/s on the book-1 random_scene, 1200x800 @ 500 spp, max_depth 50
+(BASELINE.json configs[1]; metric "Msamples/sec (whole node)").
+
+One step = one full frame through the hot path (camera rays -> ray_color bounce loop -> per-pixel
+sums in HBM).  N GPUs (torchrun, one process per GPU, RCCL): the frame's 8x8 tiles are dealt
+round-robin to ranks, each rank renders its tiles into a packed buffer and rank 0 gathers them over
+xGMI (the north star's exchange step) and scatters them into the [H][W][3] image: strong scaling of
+one frame.  Scene upload happens before the timed region; inputs are resident in HBM.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` (dominant kernel:
+the persistent trace kernel, timed with HIP events on the launch stream) and `cpu_baseline` (the f64
+C oracle on the host cores, bounded sample).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "shirley-raytracing-rs_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
+FP64_PEAK_TFLOPS = 78.6      # MI355X vector FP64 (spec)
+BYTES_PER_SEGMENT = 256      # algorithmic bytes per path segment, f64 path state
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--width", type=int, default=1200)
+    ap.add_argument("--aspect", default="std3x2")
+    ap.add_argument("--spp", type=int, default=500)
+    ap.add_argument("--max-depth", type=int, default=50)
+    ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED)
+    ap.add_argument("--scene", default="random")
+    ap.add_argument("--bvh", default="sah", choices=["reference", "sah"])
+    ap.add_argument("--sample-chunk", type=int, default=0)
+    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, cam, args):
+    """The oracle (f64 C restatement, test infrastructure) timed on the host: full frame at reduced
+    spp (Msamples/s is per-sample throughput, so the spp reduction keeps the per-sample work)."""
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib as O
+    osc = O.OracleScene(scene)
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    p = O.params(args.cpu_spp, args.max_depth, args.seed)
+    t0 = time.perf_counter()
+    _, cnt = osc.render(cam, p, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(cnt.samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{args.scene} {cam.image_width}x{cam.image_height} @ {args.cpu_spp} spp "
+                      f"({cnt.samples} samples, {dt:.1f} s wall on {threads} threads; f64 C oracle)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import raytracer as rt
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    scene = rt.SceneBuilder.builtin(args.scene, args.seed).finalize(args.seed)
+    cam = rt.scene_camera(args.scene, args.width, args.aspect)
+    W, H = cam.image_width, cam.image_height
+    dev = rt.Device(local)
+    dev.upload(scene, args.bvh)
+    settings = rt.RenderSettings(samples=args.spp, max_reflect=args.max_depth, seed=args.seed,
+                                 sample_chunk=args.sample_chunk, tile_rank=rank, tile_world=world)
+    stream = torch.cuda.current_stream()
+    sh = stream.cuda_stream
+    accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    if world > 1:
+        n_tiles, max_tiles = rt.tile_layout(cam, world)
+        packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
+        gathered = torch.zeros((world, max_tiles, 64, 3), dtype=torch.float64, device="cuda")
+
+    def step():
+        if world == 1:
+            dev.render_device(cam, settings, accum.data_ptr(), sh)
+        else:
+            dev.render_tiles_device(cam, settings, packed.data_ptr(), sh)
+            dist.all_gather_into_tensor(gathered, packed)  # RCCL over xGMI; rank 0 assembles the frame
+            if rank == 0:
+                dev.unpack_tiles_device(cam, world, gathered.data_ptr(), accum.data_ptr(), sh)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms, segments = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
+        kernel_ms.append(c.kernel_ms)
+        segments.append(c.segments)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    total_samples = W * H * args.spp * args.steps
+    value = total_samples / elapsed / 1e6
+    k_ms = float(np.mean(kernel_ms))
+    seg = float(np.mean(segments))
+    achieved = BYTES_PER_SEGMENT * seg / (k_ms * 1e-3) / 1e9
+    traffic = None
+    tfile = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tfile):
+        try:
+            tj = json.load(open(tfile))
+            if tj.get("workload") == f"{args.scene} {W}x{H} @ {args.spp}spp" and tj.get("bvh") == args.bvh:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    line = {
+        "metric": "Msamples/sec (whole node) on book-1 random_scene 1200x800 @ 500spp; 1/2/4/8 GPU",
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"{args.scene} {W}x{H} @ {args.spp}spp, max_depth {args.max_depth}, seed "
+                               f"{args.seed:#x}", "scene": args.scene, "width": W, "height": H, "spp": args.spp,
+                   "max_depth": args.max_depth, "bvh": args.bvh, "parallelism": f"tiles8x8/{world}",
+                   "segments_per_sample": round(seg / (W * H * args.spp / world), 4) if world == 1 else None},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),
+                     "bytes_per_segment": BYTES_PER_SEGMENT, "segments_per_launch": int(seg)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        line["cpu_baseline"] = cpu_baseline(scene, cam, args)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    dev.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+/*
+ * shirley_rt.h — drop-in C ABI for the reference's render hot path on MI355X.
+ *
+ * What this replaces (all paths relative to scottschroeder/shirley-raytracing-rs):
+ *   - src/main.rs:65-130        render_scene(): the rayon loop over scanlines (main.rs:92-126)
+ *   - src/raytracer/render.rs:49-70  render_scanline(frame, rng, samples, max_depth, ws, line_idx, buf)
+ *   - src/raytracer/render.rs:17-48  ray_color()  (the per-sample bounce loop)
+ *   - src/raytracer/scene/mod.rs:111-137  SceneBuilder::finalize (texture load + BBox tree build)
+ *
+ * A host (the C++ host in this repo, or a Rust crate binding this header verbatim with
+ * bindgen/#[repr(C)]) owns the scene description, the camera and the
+ * image buffer.  The library owns device memory.  Everything here is plain C: fixed-width
+ * integers, doubles, raw pointers and sizes.  No C++ types and no exceptions cross this ABI.
+ *
+ * Arithmetic is IEEE binary64 throughout, like the reference (core/math.rs:5 `type Real = f64`).
+ *
+ * Errors: every entry point returns an rt_status; rt_last_error(ctx) holds a message.
+ * Threading: one rt_ctx per device; a ctx must not be used from two host threads at once.
+ */
+#ifndef SHIRLEY_RT_H
+#define SHIRLEY_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+typedef enum rt_status {
+  RT_OK = 0,
+  RT_E_INVALID = 1,     /* bad argument / malformed scene */
+  RT_E_HIP = 2,         /* HIP runtime error (no device, launch failure, ...) */
+  RT_E_OOM = 3,         /* device allocation failed */
+  RT_E_UNSUPPORTED = 4  /* feature not compiled in / not available */
+} rt_status;
+
+/* geometry/object.rs:9-16  GeometricObject */
+enum { RT_GEOM_SPHERE = 0, RT_GEOM_RECT_XY = 1, RT_GEOM_RECT_YZ = 2, RT_GEOM_RECT_XZ = 3, RT_GEOM_RECT_BOX = 4 };
+/* material/material_type.rs:20-27  MaterialType */
+enum { RT_MAT_METAL = 0, RT_MAT_DIELECTRIC = 1, RT_MAT_LAMBERTIAN = 2, RT_MAT_DIFFUSE_LIGHT = 3, RT_MAT_FAIRY_LIGHT = 4 };
+/* material/texture/loader.rs:17-28  TextureLoader (after load: Solid / Checker / Noise / Image) */
+enum { RT_TEX_SOLID = 0, RT_TEX_CHECKER = 1, RT_TEX_PERLIN = 2, RT_TEX_IMAGE = 3 };
+/* skybox/mod.rs:11-16  SkyBox */
+enum { RT_SKY_ABOVE = 0, RT_SKY_FLAT = 1, RT_SKY_NONE = 2 };
+/* BVH builder selection for rt_scene_upload */
+enum {
+  RT_BVH_REFERENCE = 0, /* bvh/bbox_tree/constructor.rs split rules (median/midpoint on min-x/y/z, volume score) */
+  RT_BVH_SAH = 1        /* binned surface-area heuristic (performance option; same hits up to measure-zero ties) */
+};
+
+/* One scene object = SceneLoadObject{geometry, material} (scene/mod.rs:23-27). */
+typedef struct rt_object {
+  int32_t geometry; /* RT_GEOM_* */
+  int32_t material; /* index into rt_scene_desc.materials */
+  /* Sphere  (geometry/sphere.rs:11-15): cx cy cz radius (radius may be negative: sphere.rs:48,54-60)
+   * Rect    (geometry/rect.rs:45-52):   d1_min d1_max d2_min d2_max offset
+   * RectBox (geometry/rect.rs:102-130): min.x min.y min.z max.x max.y max.z (sides derived as RectBox::new) */
+  double p[6];
+} rt_object;
+
+typedef struct rt_material {
+  int32_t kind;      /* RT_MAT_* */
+  int32_t texture;   /* albedo texture (Lambertian / DiffuseLight / FairyLight), -1 otherwise */
+  double albedo[3];  /* Metal albedo (metal.rs:10-14) */
+  double param;      /* Metal: fuzz, already clamped <= 1 (metal.rs:17-23); Dielectric: ir (dielectric.rs:10-13) */
+} rt_material;
+
+typedef struct rt_texture {
+  int32_t kind;      /* RT_TEX_* */
+  int32_t odd;       /* Checker: odd child texture index  (checker.rs:10-14) */
+  int32_t even;      /* Checker: even child texture index */
+  int32_t table;     /* Perlin: index into perlin tables; Image: index into images */
+  double color[3];   /* Solid colour (solid.rs:5-21) */
+  double scale;      /* Checker: size; Perlin: scale (perlin/mod.rs:143-153) */
+} rt_texture;
+
+/* Perlin tables (perlin/mod.rs:11-17): 256 non-normalised random vectors + 3 permutations. */
+typedef struct rt_perlin_table {
+  double ranfloat[256][3];
+  int32_t perm_x[256];
+  int32_t perm_y[256];
+  int32_t perm_z[256];
+} rt_perlin_table;
+
+/* Decoded RGB8 image texture (image_texture.rs:15-17); row 0 = top, like image::DynamicImage. */
+typedef struct rt_image {
+  int32_t width;
+  int32_t height;
+  const uint8_t* rgb; /* width*height*3 bytes */
+} rt_image;
+
+/* Flattened SceneBuilder (scene/mod.rs:79-83) with textures already "loaded" and deduplicated
+ * (TextureManager::load, texture/loader.rs:113-131).  Host-owned; borrowed for the call only. */
+typedef struct rt_scene_desc {
+  int32_t sky;            /* RT_SKY_* */
+  double sky_color[3];    /* RT_SKY_FLAT colour */
+  int32_t n_objects;
+  const rt_object* objects;
+  int32_t n_materials;
+  const rt_material* materials;
+  int32_t n_textures;
+  const rt_texture* textures;
+  int32_t n_perlin;
+  const rt_perlin_table* perlin;
+  int32_t n_images;
+  const rt_image* images;
+} rt_scene_desc;
+
+/* Camera (camera/mod.rs:88-95) + CameraPosition (camera/mod.rs:63-70), as built by
+ * CameraBuilder::build (camera/mod.rs:44-60) and CameraPosition::look_at (camera/mod.rs:72-86),
+ * with the caller's `pos.focus_length = 10.0` override already applied (scenes.rs:209,229). */
+typedef struct rt_camera {
+  int32_t image_width;   /* Dimmensions.width */
+  int32_t image_height;  /* Dimmensions.height */
+  double height;         /* 2 tan(vfov/2) */
+  double width;          /* aspect * height */
+  double focal_length;
+  int32_t has_lens;      /* lens_radius: Option<f64> */
+  double lens_radius;
+  double origin[3];
+  double w[3], u[3], v[3];
+  double focus_length;
+} rt_camera;
+
+/* Per-call render parameters (RenderSettings, argparse.rs:106-123, plus what the reference lacks). */
+typedef struct rt_render_params {
+  int32_t samples;      /* samples per pixel; 0 is treated as 1 (main.rs:75-80) */
+  int32_t max_depth;    /* max_reflect: bounce limit of ray_color (render.rs:30) */
+  uint64_t seed;        /* key of the counter-based RNG (the reference is unseeded: SURVEY.md §0) */
+  int32_t tile_rank;    /* interleaved 8x8-tile sharding: this call renders tiles k with k % tile_world == tile_rank */
+  int32_t tile_world;   /* 1 = whole frame */
+  int32_t sample_chunk; /* samples per work unit (0 = automatic; >= samples gives in-order per-pixel sums) */
+  int32_t reserved;
+} rt_render_params;
+
+typedef struct rt_scene_stats {
+  int32_t n_objects;
+  int32_t n_nodes;      /* BVH nodes (leaves included), like BboxTree.tree.len()+... */
+  int32_t n_leaves;
+  int32_t depth;        /* max root-to-leaf depth */
+  int64_t device_bytes; /* scene bytes resident in HBM */
+} rt_scene_stats;
+
+/* Counters of the last render call (deterministic for a given seed). */
+typedef struct rt_counters {
+  uint64_t samples;     /* paths started = pixels x spp */
+  uint64_t segments;    /* ray_color loop iterations that traced a ray (hit + miss) */
+  uint64_t node_visits; /* BVH child-box tests */
+  uint64_t prim_tests;  /* primitive intersection calls */
+  double kernel_ms;     /* device time of the trace kernel (HIP events) */
+  double reduce_ms;     /* device time of the partial-sum reduce kernel */
+} rt_counters;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- library / device ---------------------------------------------------------------------- */
+const char* rt_version(void);
+int rt_device_count(int32_t* out);
+int rt_create(int32_t device, rt_ctx** out);
+int rt_destroy(rt_ctx* ctx);
+const char* rt_last_error(const rt_ctx* ctx);
+
+/* ---- scene (replaces SceneBuilder::finalize, scene/mod.rs:111-137) --------------------------- */
+int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene, int32_t bvh_builder);
+int rt_scene_stats_get(rt_ctx* ctx, rt_scene_stats* out);
+
+/* ---- rendering (replaces main.rs:92-126 + render.rs:17-70) ----------------------------------- */
+/* Whole frame, blocking.  accum_host: [image_height][image_width][3] f64 per-pixel SUMS over the
+ * samples (Image.data layout, image.rs:10-14), row 0 = bottom of the picture (image.rs:38). */
+int rt_render(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* params, double* accum_host);
+
+/* Rows [line_begin, line_end) only, blocking — the render_scanline (render.rs:49-57) granularity.
+ * rows_host: [(line_end-line_begin)][image_width][3] sums; samples of row j identical to rt_render's. */
+int rt_render_scanlines(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* params,
+                        int32_t line_begin, int32_t line_end, double* rows_host);
+
+/* Device-resident variants: asynchronous on `stream` (a hipStream_t, NULL = the ctx's own stream).
+ * rt_render_device: accum_dev is [H][W][3] f64 in HBM; pixels of tiles not owned by this
+ * (tile_rank, tile_world) are left untouched.
+ * rt_render_tiles_device: packed output [n_tiles_rank][8][8][3] f64 (tile-local row 0 = lowest row),
+ * for the multi-GPU gather; rt_unpack_tiles_device scatters a gathered [world][max_tiles][8][8][3]
+ * buffer back into [H][W][3]. */
+int rt_tile_layout(const rt_camera* cam, int32_t tile_world, int32_t* n_tiles_total, int32_t* max_tiles_per_rank);
+int rt_render_device(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* params, double* accum_dev,
+                     void* stream);
+int rt_render_tiles_device(rt_ctx* ctx, const rt_camera* cam, const rt_render_params* params,
+                           double* packed_dev, void* stream);
+int rt_unpack_tiles_device(rt_ctx* ctx, const rt_camera* cam, int32_t tile_world, const double* gathered_dev,
+                           double* accum_dev, void* stream);
+int rt_synchronize(rt_ctx* ctx);
+
+/* Closest hit for a batch of rays, blocking — Hittable for Scene (scene/mod.rs:180-190) /
+ * WorkspaceScene::hit_workspace (scene/mod.rs:152-164).  rays: [n][6] = origin xyz, direction xyz.
+ * out[i].object = -1 on a miss; otherwise the HitRecord (geometry/hittable.rs:6-14) of object index. */
+typedef struct rt_hit {
+  int32_t object;
+  int32_t front_face;
+  double t;
+  double point[3];
+  double normal[3];
+  double u, v;
+} rt_hit;
+int rt_scene_hit(rt_ctx* ctx, const double* rays, int32_t n, double t_min, double t_max, rt_hit* out);
+
+/* Counters (segments etc.) of the most recent render call; blocks until it finished. */
+int rt_counters_get(rt_ctx* ctx, rt_counters* out);
+
+/* Host-only BVH inspection (no device needed): builds the tree rt_scene_upload would build.
+ * Call with nodes = NULL to get *n_nodes, then again with room for that many.  Node layout follows
+ * BboxTree.tree (bbox_tree.rs:10-26): leaf >= 0 is the object index, else lhs/rhs are node indices. */
+typedef struct rt_bvh_node {
+  double box[6]; /* min xyz, max xyz */
+  int32_t leaf;
+  int32_t lhs, rhs;
+  int32_t pad;
+} rt_bvh_node;
+int rt_bvh_build_host(const rt_scene_desc* scene, int32_t bvh_builder, int32_t* n_nodes, rt_bvh_node* nodes,
+                      int32_t* root);
+
+/* Output stage on the host, exactly image::to_image (image.rs:31-44) + Color::to_pixel (color.rs:31-38):
+ * c/samples -> sqrt -> (x*255.999) saturating to u8, row j -> output row H-1-j.  rgb8: [H][W][3], row 0 = top. */
+int rt_tonemap(const double* accum, int32_t width, int32_t height, int32_t samples, uint8_t* rgb8);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SHIRLEY_RT_H */

@@ -1,0 +1,192 @@
+// main.cpp — ray-cli: the reference's CLI (src/main.rs, src/argparse.rs) on the C++ host, with
+// render_scene (main.rs:65-130) calling the MI355X render ABI instead of the rayon scanline loop.
+//
+//   ray-cli [-v...] render <random|saved|demo|perlin|earth|box-light|cornell|spheres> [options]
+//   ray-cli test
+//
+// Reference flags (argparse.rs:106-167): -o/--output out.png, -s/--samples 100, -m/--max-reflect 50,
+// --single-threaded (accepted; the GPU path has no CPU thread count), -w/--width 640, --camera-fov 20,
+// --camera-focal-length 1.0, --camera-aperture 0.001, --camera-aspect-ratio std3x2;
+// random: --night, --scene-output FILE; saved: <scene_input>.
+// Added: --seed N (the reference is unseeded), --device N, --bvh reference|sah, --sample-chunk N,
+// --dump-accum FILE (raw f64 [H][W][3] sums, row 0 = bottom), --side-len N (spheres).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../../include/shirley_host.h"
+#include "../../../include/shirley_rt.h"
+
+namespace {
+
+int verbose = 0;
+
+struct Args {
+  std::string scene, output = "out.png", scene_output, scene_input, dump_accum, aspect = "std3x2", bvh = "reference";
+  int samples = 100, max_reflect = 50, width = 640, device = 0, sample_chunk = 0, side_len = 11;
+  double fov = 20.0, focal = 1.0, aperture = 0.001;
+  bool night = false, single_threaded = false;
+  unsigned long long seed = 0x5EED;
+};
+
+[[noreturn]] void usage(const char* msg) {
+  if (msg && *msg) std::fprintf(stderr, "error: %s\n", msg);
+  std::fprintf(stderr,
+               "usage: ray-cli [-v] render <random|saved|demo|perlin|earth|box-light|cornell|spheres> [options]\n"
+               "       ray-cli test\n"
+               "options: -o FILE -s N -m N -w N --single-threaded --camera-fov F --camera-focal-length F\n"
+               "         --camera-aperture F --camera-aspect-ratio std3x2|std16x9|std16x10|square|target-iphone\n"
+               "         --night --scene-output FILE (random)  <scene_input> (saved)  --side-len N (spheres)\n"
+               "         --seed N --device N --bvh reference|sah --sample-chunk N --dump-accum FILE\n");
+  std::exit(2);
+}
+
+int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam) {
+  int samples = a.samples;
+  if (samples == 0) {  // main.rs:75-80
+    std::fprintf(stderr, "WARN samples set to 0, using 1\n");
+    samples = 1;
+  }
+  rt_ctx* ctx = nullptr;
+  int st = rt_create(a.device, &ctx);
+  if (st) {
+    std::fprintf(stderr, "error: rt_create(device %d) failed (%d): no usable MI355X device?\n", a.device, st);
+    return 1;
+  }
+  int builder = a.bvh == "sah" ? RT_BVH_SAH : RT_BVH_REFERENCE;
+  auto t0 = std::chrono::steady_clock::now();
+  if ((st = rt_scene_upload(ctx, desc, builder))) {
+    std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
+    rt_destroy(ctx);
+    return 1;
+  }
+  rt_render_params p{};
+  p.samples = samples;
+  p.max_depth = a.max_reflect;
+  p.seed = a.seed;
+  p.tile_rank = 0;
+  p.tile_world = 1;
+  p.sample_chunk = a.sample_chunk;
+  std::vector<double> accum((size_t)cam.image_width * cam.image_height * 3);
+  auto t1 = std::chrono::steady_clock::now();
+  if ((st = rt_render(ctx, &cam, &p, accum.data()))) {
+    std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
+    rt_destroy(ctx);
+    return 1;
+  }
+  auto t2 = std::chrono::steady_clock::now();
+  rt_counters cnt{};
+  rt_counters_get(ctx, &cnt);
+  double ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  double msamp = (double)cam.image_width * cam.image_height * samples / (cnt.kernel_ms * 1e3);
+  if (verbose >= 1)
+    std::fprintf(stderr,
+                 "INFO upload %.1f ms, render %.1f ms (kernel %.2f ms, reduce %.3f ms): %.1f Msamples/s, %.3f segments/sample\n",
+                 std::chrono::duration<double, std::milli>(t1 - t0).count(), ms, cnt.kernel_ms, cnt.reduce_ms, msamp,
+                 (double)cnt.segments / (double)(cnt.samples ? cnt.samples : 1));
+  rt_destroy(ctx);
+  if (!a.dump_accum.empty()) {
+    std::ofstream f(a.dump_accum, std::ios::binary);
+    f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
+  }
+  std::vector<uint8_t> rgb(accum.size());
+  rt_tonemap(accum.data(), cam.image_width, cam.image_height, samples, rgb.data());  // image.rs:31-44
+  if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
+    std::fprintf(stderr, "error: %s\n", sh_last_error());
+    return 1;
+  }
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) usage(("missing value for " + s).c_str());
+      return argv[++i];
+    };
+    if (s == "-v" || s == "--verbose") ++verbose;
+    else if (s.size() > 2 && s[0] == '-' && s[1] == 'v' && s.find_first_not_of('v', 1) == std::string::npos) verbose += (int)s.size() - 1;
+    else if (s == "-o" || s == "--output") a.output = next();
+    else if (s == "-s" || s == "--samples") a.samples = std::atoi(next().c_str());
+    else if (s == "-m" || s == "--max-reflect") a.max_reflect = std::atoi(next().c_str());
+    else if (s == "--single-threaded") a.single_threaded = true;
+    else if (s == "-w" || s == "--width") a.width = std::atoi(next().c_str());
+    else if (s == "--camera-fov") a.fov = std::atof(next().c_str());
+    else if (s == "--camera-focal-length") a.focal = std::atof(next().c_str());
+    else if (s == "--camera-aperture") a.aperture = std::atof(next().c_str());
+    else if (s == "--camera-aspect-ratio") a.aspect = next();
+    else if (s == "--night") a.night = true;
+    else if (s == "--scene-output") a.scene_output = next();
+    else if (s == "--seed") a.seed = std::strtoull(next().c_str(), nullptr, 0);
+    else if (s == "--device") a.device = std::atoi(next().c_str());
+    else if (s == "--bvh") a.bvh = next();
+    else if (s == "--sample-chunk") a.sample_chunk = std::atoi(next().c_str());
+    else if (s == "--dump-accum") a.dump_accum = next();
+    else if (s == "--side-len") a.side_len = std::atoi(next().c_str());
+    else if (s == "-h" || s == "--help") usage("");
+    else if (!s.empty() && s[0] == '-') usage(("unknown option " + s).c_str());
+    else pos.push_back(s);
+  }
+  if (pos.empty()) usage("missing subcommand");
+  if (pos[0] == "test") {  // main.rs:60-63
+    std::fprintf(stderr, "ERROR there is nothing to test!\n");
+    return 0;
+  }
+  if (pos[0] != "render" || pos.size() < 2) usage("expected `render <scene>`");
+  a.scene = pos[1];
+  if (a.samples < 0 || a.max_reflect < 0 || a.width < 1) usage("samples / max-reflect / width out of range");
+
+  sh_scene* scene = nullptr;
+  std::string cam_scene = a.scene;
+  if (a.scene == "saved") {
+    if (pos.size() < 3) usage("render saved needs <scene_input>");
+    std::ifstream f(pos[2]);
+    if (!f) usage(("cannot open " + pos[2]).c_str());
+    std::stringstream ss;
+    ss << f.rdbuf();
+    if (sh_scene_from_json(ss.str().c_str(), &scene)) {
+      std::fprintf(stderr, "error: %s\n", sh_last_error());
+      return 1;
+    }
+  } else {
+    std::string name = a.scene;
+    if (name == "random" && a.night) name = "random-night";
+    if (name == "spheres") name = "spheres:" + std::to_string(a.side_len);
+    if (sh_scene_builtin(name.c_str(), a.seed, &scene)) {
+      std::fprintf(stderr, "error: %s\n", sh_last_error());
+      return 1;
+    }
+  }
+  if (!a.scene_output.empty()) {  // scenes.rs:140-143
+    size_t need = 0;
+    sh_scene_to_json(scene, 1, nullptr, 0, &need);
+    std::string buf(need, '\0');
+    sh_scene_to_json(scene, 1, &buf[0], need, &need);
+    std::ofstream f(a.scene_output);
+    f << buf.c_str();
+  }
+  sh_desc* desc = nullptr;
+  if (sh_scene_finalize(scene, a.seed, &desc)) {
+    std::fprintf(stderr, "error: %s\n", sh_last_error());
+    return 1;
+  }
+  rt_camera cam{};
+  if (sh_scene_camera(cam_scene.c_str(), a.width, a.aspect.c_str(), a.fov, a.focal, a.aperture, &cam)) {
+    std::fprintf(stderr, "error: %s\n", sh_last_error());
+    return 1;
+  }
+  int rc = render_scene(a, sh_desc_view(desc), cam);
+  sh_desc_free(desc);
+  sh_scene_free(scene);
+  return rc;
+}

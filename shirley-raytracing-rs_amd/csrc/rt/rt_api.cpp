@@ -1,0 +1,656 @@
+// rt_api.cpp — implementation of the C ABI in include/shirley_rt.h.
+//
+// Host side of the boundary: validates the flattened scene, builds the BBox tree, lays the scene
+// out in HBM (rt_layout.h), sizes the persistent launch and runs trace -> reduce on a HIP stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../../include/shirley_rt.h"
+#include "bvh_build.h"
+#include "rt_layout.h"
+
+namespace rt {
+size_t trace_lds_bytes(int stack_depth);
+hipError_t trace_occupancy(int stack_depth, int* blocks_per_cu);
+hipError_t launch_trace(const KParams& p, int blocks, hipStream_t stream);
+hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
+                         int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
+hipError_t launch_unpack(const double* gathered, int world, int max_tiles, int n_tiles_total, int tiles_x, int width,
+                         int height, double* out, hipStream_t stream);
+hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, double t_max, void* out,
+                      hipStream_t stream);
+}  // namespace rt
+
+using namespace rt;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct rt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int cu_count = 0;
+  // scene
+  bool have_scene = false;
+  DScene scene{};
+  DevBuf nodes, prims, mats, texs, perlin, images, texels;
+  rt_scene_stats stats{};
+  int blocks_per_cu = 0;
+  // per-render scratch
+  DevBuf partial, accum, counters, unit_counter;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  bool have_timing = false;
+};
+
+namespace {
+
+int fail(rt_ctx* c, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return code;
+}
+
+#define HIP_TRY(ctx, expr)                                                                      \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return fail(ctx, e_ == hipErrorOutOfMemory ? RT_E_OOM : RT_E_HIP, "%s: %s (%s:%d)", #expr, \
+                  hipGetErrorString(e_), __FILE__, __LINE__);                                   \
+  } while (0)
+
+int ensure(rt_ctx* c, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return RT_OK;
+  if (b.p) {
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  if (bytes == 0) return RT_OK;
+  HIP_TRY(c, hipMalloc(&b.p, bytes));
+  b.bytes = bytes;
+  return RT_OK;
+}
+
+void release(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+int upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes) {
+  int st = ensure(c, b, std::max<size_t>(bytes, 16));
+  if (st) return st;
+  if (bytes) HIP_TRY(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+  return RT_OK;
+}
+
+// object -> leaf box, exactly the reference's bounding_box (sphere.rs:54-60, rect.rs:82-99, rect.rs:158-163)
+Box object_box(const rt_object& o) {
+  Box b{};
+  if (o.geometry == RT_GEOM_SPHERE) {
+    for (int k = 0; k < 3; ++k) {
+      b.mn[k] = o.p[k] - o.p[3];
+      b.mx[k] = o.p[k] + o.p[3];
+    }
+  } else if (o.geometry == RT_GEOM_RECT_BOX) {
+    for (int k = 0; k < 3; ++k) {
+      b.mn[k] = o.p[k];
+      b.mx[k] = o.p[k + 3];
+    }
+  } else {
+    int D1 = (o.geometry == RT_GEOM_RECT_YZ) ? 1 : 0;
+    int D2 = (o.geometry == RT_GEOM_RECT_XY) ? 1 : 2;
+    int n = 3 - D1 - D2;
+    b.mn[D1] = o.p[0];
+    b.mx[D1] = o.p[1];
+    b.mn[D2] = o.p[2];
+    b.mx[D2] = o.p[3];
+    b.mn[n] = o.p[4] - 0.0001;  // BBOX_WIDTH, rect.rs:9
+    b.mx[n] = o.p[4] + 0.0001;
+  }
+  return b;
+}
+
+int validate(rt_ctx* c, const rt_scene_desc* d) {
+  if (!d) return fail(c, RT_E_INVALID, "scene is NULL");
+  if (d->n_objects < 0 || d->n_materials < 0 || d->n_textures < 0 || d->n_perlin < 0 || d->n_images < 0)
+    return fail(c, RT_E_INVALID, "negative count in scene");
+  if ((d->n_objects && !d->objects) || (d->n_materials && !d->materials) || (d->n_textures && !d->textures) ||
+      (d->n_perlin && !d->perlin) || (d->n_images && !d->images))
+    return fail(c, RT_E_INVALID, "NULL array with non-zero count");
+  if (d->sky < RT_SKY_ABOVE || d->sky > RT_SKY_NONE) return fail(c, RT_E_INVALID, "bad skybox %d", d->sky);
+  for (int i = 0; i < d->n_objects; ++i) {
+    const rt_object& o = d->objects[i];
+    if (o.geometry < RT_GEOM_SPHERE || o.geometry > RT_GEOM_RECT_BOX)
+      return fail(c, RT_E_INVALID, "object %d: bad geometry %d", i, o.geometry);
+    if (o.material < 0 || o.material >= d->n_materials)
+      return fail(c, RT_E_INVALID, "object %d: material %d out of range", i, o.material);
+  }
+  for (int i = 0; i < d->n_materials; ++i) {
+    const rt_material& m = d->materials[i];
+    if (m.kind < RT_MAT_METAL || m.kind > RT_MAT_FAIRY_LIGHT)
+      return fail(c, RT_E_INVALID, "material %d: bad kind %d", i, m.kind);
+    bool textured = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT || m.kind == RT_MAT_FAIRY_LIGHT;
+    if (textured && (m.texture < 0 || m.texture >= d->n_textures))
+      return fail(c, RT_E_INVALID, "material %d: texture %d out of range", i, m.texture);
+  }
+  for (int i = 0; i < d->n_textures; ++i) {
+    const rt_texture& t = d->textures[i];
+    switch (t.kind) {
+      case RT_TEX_SOLID: break;
+      case RT_TEX_CHECKER:
+        if (t.odd < 0 || t.odd >= d->n_textures || t.even < 0 || t.even >= d->n_textures)
+          return fail(c, RT_E_INVALID, "texture %d: checker child out of range", i);
+        // children must be earlier textures: guarantees the lookup terminates (no cycles)
+        if (t.odd >= i || t.even >= i) return fail(c, RT_E_INVALID, "texture %d: checker children must precede it", i);
+        break;
+      case RT_TEX_PERLIN:
+        if (t.table < 0 || t.table >= d->n_perlin) return fail(c, RT_E_INVALID, "texture %d: perlin table", i);
+        break;
+      case RT_TEX_IMAGE:
+        if (t.table < 0 || t.table >= d->n_images) return fail(c, RT_E_INVALID, "texture %d: image index", i);
+        break;
+      default: return fail(c, RT_E_INVALID, "texture %d: bad kind %d", i, t.kind);
+    }
+  }
+  for (int i = 0; i < d->n_perlin; ++i)
+    for (int k = 0; k < 256; ++k) {
+      const rt_perlin_table& T = d->perlin[i];
+      if (T.perm_x[k] < 0 || T.perm_x[k] > 255 || T.perm_y[k] < 0 || T.perm_y[k] > 255 || T.perm_z[k] < 0 ||
+          T.perm_z[k] > 255)
+        return fail(c, RT_E_INVALID, "perlin table %d: permutation entry out of [0,255]", i);
+    }
+  for (int i = 0; i < d->n_images; ++i)
+    if (d->images[i].width < 1 || d->images[i].height < 1 || !d->images[i].rgb)
+      return fail(c, RT_E_INVALID, "image %d: empty", i);
+  return RT_OK;
+}
+
+BuiltTree build_tree(const rt_scene_desc* d, int32_t builder) {
+  std::vector<Box> boxes(d->n_objects);
+  for (int i = 0; i < d->n_objects; ++i) boxes[i] = object_box(d->objects[i]);
+  return builder == RT_BVH_SAH ? build_sah_tree(boxes) : build_reference_tree(boxes);
+}
+
+void box_to6(const Box& b, double* o) {
+  for (int k = 0; k < 3; ++k) {
+    o[k] = b.mn[k];
+    o[k + 3] = b.mx[k];
+  }
+}
+
+// BuiltTree -> DNode array in depth-first order: node 0 = top node whose child 0 is the root.
+void flatten(const BuiltTree& t, std::vector<DNode>& out) {
+  out.clear();
+  DNode top{};
+  top.child[0] = kEmptyChild;
+  top.child[1] = kEmptyChild;
+  for (int k = 0; k < 6; ++k) top.box[1][k] = (k < 3) ? INFINITY : -INFINITY;
+  out.push_back(top);
+  if (t.root < 0) {
+    for (int k = 0; k < 6; ++k) out[0].box[0][k] = (k < 3) ? INFINITY : -INFINITY;
+    return;
+  }
+  // child reference for a BuiltTree node: ~object for a leaf, else the DNode index (assigned on visit)
+  struct Item {
+    int32_t built;
+    int32_t parent;
+    int slot;
+  };
+  std::vector<Item> st{{t.root, 0, 0}};
+  while (!st.empty()) {
+    Item it = st.back();
+    st.pop_back();
+    const BuildNode& bn = t.nodes[it.built];
+    box_to6(bn.box, out[it.parent].box[it.slot]);
+    if (bn.leaf >= 0) {
+      out[it.parent].child[it.slot] = ~bn.leaf;
+      continue;
+    }
+    int32_t idx = (int32_t)out.size();
+    out[it.parent].child[it.slot] = idx;
+    DNode n{};
+    out.push_back(n);
+    st.push_back({bn.rhs, idx, 1});
+    st.push_back({bn.lhs, idx, 0});
+  }
+}
+
+int resolve_stream(rt_ctx* c, void* stream, hipStream_t* out) {
+  *out = stream ? reinterpret_cast<hipStream_t>(stream) : c->stream;
+  return RT_OK;
+}
+
+struct Layout {
+  int tiles_x, tiles_y, n_tiles, n_tiles_rank;
+};
+
+Layout layout(const rt_camera* cam, int ty0, int ty1, int rank, int world) {
+  Layout L;
+  L.tiles_x = (cam->image_width + kTile - 1) / kTile;
+  L.tiles_y = ty1 - ty0;
+  L.n_tiles = L.tiles_x * L.tiles_y;
+  L.n_tiles_rank = (L.n_tiles > rank) ? (L.n_tiles - rank + world - 1) / world : 0;
+  return L;
+}
+
+DCamera device_camera(const rt_camera* c) {
+  // camera/mod.rs:99-108, evaluated once with the reference's operation order (-ffp-contract=off)
+  DCamera d{};
+  d.width = c->image_width;
+  d.height = c->image_height;
+  d.has_lens = c->has_lens;
+  d.lens_radius = c->lens_radius;
+  for (int k = 0; k < 3; ++k) {
+    d.origin[k] = c->origin[k];
+    d.u[k] = c->u[k];
+    d.v[k] = c->v[k];
+    d.horizontal[k] = c->u[k] * (c->width * c->focus_length);
+    d.vertical[k] = c->v[k] * (c->height * c->focus_length);
+  }
+  for (int k = 0; k < 3; ++k)
+    d.lower_left[k] = ((c->origin[k] - d.horizontal[k] * 0.5) - d.vertical[k] * 0.5) -
+                      c->w[k] * (c->focal_length * c->focus_length);
+  return d;
+}
+
+int check_render_args(rt_ctx* c, const rt_camera* cam, const rt_render_params* p) {
+  if (!c) return RT_E_INVALID;
+  if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded (call rt_scene_upload first)");
+  if (!cam || !p) return fail(c, RT_E_INVALID, "camera/params is NULL");
+  if (cam->image_width < 1 || cam->image_height < 1 || cam->image_width > (1 << 16) || cam->image_height > (1 << 16))
+    return fail(c, RT_E_INVALID, "bad image size %dx%d", cam->image_width, cam->image_height);
+  if (p->samples < 0 || p->max_depth < 0) return fail(c, RT_E_INVALID, "negative samples/max_depth");
+  if (p->tile_world < 1 || p->tile_rank < 0 || p->tile_rank >= p->tile_world)
+    return fail(c, RT_E_INVALID, "bad tile rank/world %d/%d", p->tile_rank, p->tile_world);
+  if (p->sample_chunk < 0) return fail(c, RT_E_INVALID, "negative sample_chunk");
+  return RT_OK;
+}
+
+// trace + reduce for tile rows [ty0, ty1) ; out layout: packed tiles (packed=1) or rows [row0,row1)
+int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int ty0, int ty1, int row0, int row1,
+                  int packed, double* out_dev, hipStream_t s) {
+  int st = check_render_args(c, cam, p);
+  if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const int samples = p->samples == 0 ? 1 : p->samples;  // main.rs:75-80
+  Layout L = layout(cam, ty0, ty1, p->tile_rank, p->tile_world);
+  const long long n_pix = (long long)L.n_tiles_rank * kTilePixels;
+
+  // samples per unit: enough units to keep every resident lane busy ~16x over (tail < ~3%)
+  int chunk = p->sample_chunk;
+  if (chunk == 0) {
+    long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * kBlockThreads;
+    long long want_units = 16 * lanes;
+    long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
+    n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
+    chunk = (int)((samples + n_chunks - 1) / n_chunks);
+  }
+  chunk = std::max(1, std::min(chunk, samples));
+  const int n_chunks = (samples + chunk - 1) / chunk;
+
+  st = ensure(c, c->partial, (size_t)std::max<long long>(1, n_pix * n_chunks * 3) * sizeof(double));
+  if (st) return st;
+
+  KParams kp{};
+  kp.scene = c->scene;
+  kp.cam = device_camera(cam);
+  kp.work.tiles_x = L.tiles_x;
+  kp.work.tiles_y = L.tiles_y;
+  kp.work.ty0 = ty0;
+  kp.work.tile_rank = p->tile_rank;
+  kp.work.tile_world = p->tile_world;
+  kp.work.n_tiles_rank = L.n_tiles_rank;
+  kp.work.samples = samples;
+  kp.work.chunk = chunk;
+  kp.work.n_chunks = n_chunks;
+  kp.work.max_depth = p->max_depth;
+  kp.work.seed = p->seed;
+  kp.work.n_units = (uint64_t)n_pix * (uint64_t)n_chunks;
+  kp.partial = static_cast<double*>(c->partial.p);
+  kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
+  kp.counters = static_cast<DCounters*>(c->counters.p);
+
+  HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
+  HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, sizeof(DCounters), s));
+  const int blocks = std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
+  HIP_TRY(c, hipEventRecord(c->ev[0], s));
+  if (n_pix > 0) HIP_TRY(c, launch_trace(kp, blocks, s));
+  HIP_TRY(c, hipEventRecord(c->ev[1], s));
+  if (n_pix > 0)
+    HIP_TRY(c, launch_reduce(kp.partial, n_chunks, L.n_tiles_rank, L.tiles_x, ty0, p->tile_rank, p->tile_world,
+                             cam->image_width, row0, row1, packed, out_dev, s));
+  HIP_TRY(c, hipEventRecord(c->ev[2], s));
+  c->have_timing = true;
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_version(void) { return "shirley-rt 0.1 (gfx950, f64 persistent megakernel)"; }
+
+int rt_device_count(int32_t* out) {
+  if (!out) return RT_E_INVALID;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  *out = (e == hipSuccess) ? n : 0;
+  return e == hipSuccess ? RT_OK : RT_E_HIP;
+}
+
+const char* rt_last_error(const rt_ctx* ctx) { return ctx ? ctx->err.c_str() : "NULL context"; }
+
+int rt_create(int32_t device, rt_ctx** out) {
+  if (!out) return RT_E_INVALID;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return RT_E_HIP;
+  if (device < 0 || device >= n) return RT_E_INVALID;
+  rt_ctx* c = new rt_ctx();
+  c->device = device;
+  auto bail = [&](int code) {
+    rt_destroy(c);
+    return code;
+  };
+  if (hipSetDevice(device) != hipSuccess) return bail(RT_E_HIP);
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(RT_E_HIP);
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return bail(RT_E_HIP);
+  c->cu_count = prop.multiProcessorCount;
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(RT_E_HIP);
+  if (ensure(c, c->counters, sizeof(DCounters)) || ensure(c, c->unit_counter, 64)) return bail(RT_E_OOM);
+  *out = c;
+  return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+  if (!c) return RT_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (DevBuf* b : {&c->nodes, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->partial,
+                    &c->accum, &c->counters, &c->unit_counter})
+    release(*b);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return RT_OK;
+}
+
+int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
+  if (!c) return RT_E_INVALID;
+  int st = validate(c, d);
+  if (st) return st;
+  if (builder != RT_BVH_REFERENCE && builder != RT_BVH_SAH) return fail(c, RT_E_INVALID, "bad bvh builder %d", builder);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  c->have_scene = false;
+
+  BuiltTree tree = build_tree(d, builder);
+  std::vector<DNode> nodes;
+  flatten(tree, nodes);
+  std::vector<DPrim> prims(std::max(1, d->n_objects));
+  for (int i = 0; i < d->n_objects; ++i) {
+    const rt_object& o = d->objects[i];
+    DPrim& q = prims[i];
+    std::memset(&q, 0, sizeof q);
+    for (int k = 0; k < 6; ++k) q.p[k] = o.p[k];
+    q.kind = o.geometry == RT_GEOM_SPHERE     ? kPrimSphere
+             : o.geometry == RT_GEOM_RECT_XY  ? kPrimRectXY
+             : o.geometry == RT_GEOM_RECT_YZ  ? kPrimRectYZ
+             : o.geometry == RT_GEOM_RECT_XZ  ? kPrimRectXZ
+                                              : kPrimBox;
+    q.material = o.material;
+  }
+  std::vector<DMat> mats(std::max(1, d->n_materials));
+  for (int i = 0; i < d->n_materials; ++i) {
+    const rt_material& m = d->materials[i];
+    DMat& q = mats[i];
+    std::memset(&q, 0, sizeof q);
+    q.kind = m.kind;
+    q.tex = m.texture;
+    for (int k = 0; k < 3; ++k) q.albedo[k] = m.albedo[k];
+    q.param = m.param;
+  }
+  std::vector<DTex> texs(std::max(1, d->n_textures));
+  for (int i = 0; i < d->n_textures; ++i) {
+    const rt_texture& t = d->textures[i];
+    DTex& q = texs[i];
+    std::memset(&q, 0, sizeof q);
+    q.kind = t.kind;
+    q.odd = t.odd;
+    q.even = t.even;
+    q.table = t.table;
+    for (int k = 0; k < 3; ++k) q.color[k] = t.color[k];
+    q.scale = t.scale;
+  }
+  std::vector<DPerlin> perl(std::max(1, d->n_perlin));
+  for (int i = 0; i < d->n_perlin; ++i) {
+    std::memcpy(perl[i].ranfloat, d->perlin[i].ranfloat, sizeof perl[i].ranfloat);
+    std::memcpy(perl[i].perm_x, d->perlin[i].perm_x, sizeof perl[i].perm_x);
+    std::memcpy(perl[i].perm_y, d->perlin[i].perm_y, sizeof perl[i].perm_y);
+    std::memcpy(perl[i].perm_z, d->perlin[i].perm_z, sizeof perl[i].perm_z);
+  }
+  std::vector<DImage> imgs(std::max(1, d->n_images));
+  std::vector<uint8_t> texels;
+  for (int i = 0; i < d->n_images; ++i) {
+    imgs[i].width = d->images[i].width;
+    imgs[i].height = d->images[i].height;
+    imgs[i].offset = (int64_t)texels.size();
+    size_t nb = (size_t)d->images[i].width * d->images[i].height * 3;
+    texels.insert(texels.end(), d->images[i].rgb, d->images[i].rgb + nb);
+  }
+  if (texels.empty()) texels.resize(16);
+
+  if ((st = upload(c, c->nodes, nodes.data(), nodes.size() * sizeof(DNode)))) return st;
+  if ((st = upload(c, c->prims, prims.data(), prims.size() * sizeof(DPrim)))) return st;
+  if ((st = upload(c, c->mats, mats.data(), mats.size() * sizeof(DMat)))) return st;
+  if ((st = upload(c, c->texs, texs.data(), texs.size() * sizeof(DTex)))) return st;
+  if ((st = upload(c, c->perlin, perl.data(), perl.size() * sizeof(DPerlin)))) return st;
+  if ((st = upload(c, c->images, imgs.data(), imgs.size() * sizeof(DImage)))) return st;
+  if ((st = upload(c, c->texels, texels.data(), texels.size()))) return st;
+
+  DScene& S = c->scene;
+  S.nodes = static_cast<const DNode*>(c->nodes.p);
+  S.prims = static_cast<const DPrim*>(c->prims.p);
+  S.mats = static_cast<const DMat*>(c->mats.p);
+  S.texs = static_cast<const DTex*>(c->texs.p);
+  S.perlin = static_cast<const DPerlin*>(c->perlin.p);
+  S.images = static_cast<const DImage*>(c->images.p);
+  S.texels = static_cast<const uint8_t*>(c->texels.p);
+  S.n_nodes = (int32_t)nodes.size();
+  S.n_prims = d->n_objects;
+  int32_t depth = tree_branch_depth(tree);
+  S.stack_depth = depth + 2;  // ordered traversal holds at most one deferred child per branch level
+  S.sky = d->sky;
+  for (int k = 0; k < 3; ++k) S.sky_color[k] = d->sky_color[k];
+
+  int bpc = 0;
+  HIP_TRY(c, trace_occupancy(S.stack_depth, &bpc));
+  if (bpc < 1) return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
+  c->blocks_per_cu = bpc;
+
+  c->stats.n_objects = d->n_objects;
+  c->stats.n_nodes = (int32_t)tree.nodes.size();
+  int32_t leaves = 0;
+  for (const auto& n : tree.nodes) leaves += n.leaf >= 0;
+  c->stats.n_leaves = leaves;
+  c->stats.depth = depth;
+  c->stats.device_bytes = (int64_t)(nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim) +
+                                    mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex) +
+                                    perl.size() * sizeof(DPerlin) + imgs.size() * sizeof(DImage) + texels.size());
+  c->have_scene = true;
+  return RT_OK;
+}
+
+int rt_scene_stats_get(rt_ctx* c, rt_scene_stats* out) {
+  if (!c || !out) return RT_E_INVALID;
+  if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded");
+  *out = c->stats;
+  return RT_OK;
+}
+
+int rt_tile_layout(const rt_camera* cam, int32_t world, int32_t* n_tiles_total, int32_t* max_tiles_per_rank) {
+  if (!cam || world < 1 || cam->image_width < 1 || cam->image_height < 1) return RT_E_INVALID;
+  int tiles_y = (cam->image_height + kTile - 1) / kTile;
+  Layout L = layout(cam, 0, tiles_y, 0, world);
+  if (n_tiles_total) *n_tiles_total = L.n_tiles;
+  if (max_tiles_per_rank) *max_tiles_per_rank = (L.n_tiles + world - 1) / world;
+  return RT_OK;
+}
+
+int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, double* accum_dev, void* stream) {
+  if (!accum_dev) return fail(c, RT_E_INVALID, "accum_dev is NULL");
+  hipStream_t s;
+  resolve_stream(c, stream, &s);
+  int tiles_y = cam ? (cam->image_height + kTile - 1) / kTile : 0;
+  return render_window(c, cam, p, 0, tiles_y, 0, cam ? cam->image_height : 0, 0, accum_dev, s);
+}
+
+int rt_render_tiles_device(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, double* packed_dev,
+                           void* stream) {
+  if (!packed_dev) return fail(c, RT_E_INVALID, "packed_dev is NULL");
+  hipStream_t s;
+  resolve_stream(c, stream, &s);
+  int tiles_y = cam ? (cam->image_height + kTile - 1) / kTile : 0;
+  return render_window(c, cam, p, 0, tiles_y, 0, cam ? cam->image_height : 0, 1, packed_dev, s);
+}
+
+int rt_unpack_tiles_device(rt_ctx* c, const rt_camera* cam, int32_t world, const double* gathered_dev,
+                           double* accum_dev, void* stream) {
+  if (!c || !cam || !gathered_dev || !accum_dev || world < 1) return fail(c, RT_E_INVALID, "bad unpack args");
+  hipStream_t s;
+  resolve_stream(c, stream, &s);
+  int32_t n_total = 0, max_tiles = 0;
+  rt_tile_layout(cam, world, &n_total, &max_tiles);
+  int tiles_x = (cam->image_width + kTile - 1) / kTile;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, launch_unpack(gathered_dev, world, max_tiles, n_total, tiles_x, cam->image_width, cam->image_height,
+                           accum_dev, s));
+  return RT_OK;
+}
+
+int rt_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, double* accum_host) {
+  if (!c) return RT_E_INVALID;
+  if (!accum_host || !cam) return fail(c, RT_E_INVALID, "NULL argument");
+  return rt_render_scanlines(c, cam, p, 0, cam->image_height, accum_host);
+}
+
+int rt_render_scanlines(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int32_t line_begin,
+                        int32_t line_end, double* rows_host) {
+  if (!c) return RT_E_INVALID;
+  if (!cam || !rows_host) return fail(c, RT_E_INVALID, "NULL argument");
+  if (line_begin < 0 || line_end > cam->image_height || line_begin > line_end)
+    return fail(c, RT_E_INVALID, "bad line range [%d, %d)", line_begin, line_end);
+  if (line_begin == line_end) return RT_OK;
+  if (p && p->tile_world != 1) return fail(c, RT_E_INVALID, "host-buffer render needs tile_world == 1");
+  size_t bytes = (size_t)(line_end - line_begin) * cam->image_width * 3 * sizeof(double);
+  int st = ensure(c, c->accum, bytes);
+  if (st) return st;
+  int ty0 = line_begin / kTile, ty1 = (line_end + kTile - 1) / kTile;
+  st = render_window(c, cam, p, ty0, ty1, line_begin, line_end, 0, static_cast<double*>(c->accum.p), c->stream);
+  if (st) return st;
+  HIP_TRY(c, hipMemcpyAsync(rows_host, c->accum.p, bytes, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return RT_OK;
+}
+
+int rt_scene_hit(rt_ctx* c, const double* rays, int32_t n, double t_min, double t_max, rt_hit* out) {
+  if (!c) return RT_E_INVALID;
+  if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded");
+  if (n < 0 || (n > 0 && (!rays || !out))) return fail(c, RT_E_INVALID, "bad ray batch");
+  if (n == 0) return RT_OK;
+  static_assert(sizeof(rt_hit) == 80, "rt_hit layout");
+  HIP_TRY(c, hipSetDevice(c->device));
+  DevBuf r, h;
+  int st = upload(c, r, rays, (size_t)n * 6 * sizeof(double));
+  if (!st) st = ensure(c, h, (size_t)n * sizeof(rt_hit));
+  if (!st) {
+    hipError_t e = launch_hit(c->scene, static_cast<const double*>(r.p), n, t_min, t_max, h.p, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, h.p, (size_t)n * sizeof(rt_hit), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) st = fail(c, RT_E_HIP, "rt_scene_hit: %s", hipGetErrorString(e));
+  }
+  release(r);
+  release(h);
+  return st;
+}
+
+int rt_synchronize(rt_ctx* c) {
+  if (!c) return RT_E_INVALID;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipDeviceSynchronize());
+  return RT_OK;
+}
+
+int rt_counters_get(rt_ctx* c, rt_counters* out) {
+  if (!c || !out) return RT_E_INVALID;
+  std::memset(out, 0, sizeof *out);
+  if (!c->have_timing) return fail(c, RT_E_INVALID, "no render has run on this context");
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipEventSynchronize(c->ev[2]));
+  DCounters dc;
+  HIP_TRY(c, hipMemcpy(&dc, c->counters.p, sizeof dc, hipMemcpyDeviceToHost));
+  out->samples = dc.samples;
+  out->segments = dc.segments;
+  out->node_visits = dc.node_visits;
+  out->prim_tests = dc.prim_tests;
+  float a = 0.f, b = 0.f;
+  HIP_TRY(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+  HIP_TRY(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+  out->kernel_ms = a;
+  out->reduce_ms = b;
+  return RT_OK;
+}
+
+int rt_bvh_build_host(const rt_scene_desc* d, int32_t builder, int32_t* n_nodes, rt_bvh_node* nodes, int32_t* root) {
+  if (!d || !n_nodes) return RT_E_INVALID;
+  if (validate(nullptr, d)) return RT_E_INVALID;
+  BuiltTree t = build_tree(d, builder);
+  if (nodes) {
+    if (*n_nodes < (int32_t)t.nodes.size()) return RT_E_INVALID;
+    for (size_t i = 0; i < t.nodes.size(); ++i) {
+      box_to6(t.nodes[i].box, nodes[i].box);
+      nodes[i].leaf = t.nodes[i].leaf;
+      nodes[i].lhs = t.nodes[i].lhs;
+      nodes[i].rhs = t.nodes[i].rhs;
+      nodes[i].pad = 0;
+    }
+  }
+  *n_nodes = (int32_t)t.nodes.size();
+  if (root) *root = t.root;
+  return RT_OK;
+}
+
+int rt_tonemap(const double* accum, int32_t width, int32_t height, int32_t samples, uint8_t* rgb8) {
+  if (!accum || !rgb8 || width < 1 || height < 1) return RT_E_INVALID;
+  const double inv = 1.0 / (double)(samples == 0 ? 1 : samples);
+  for (int32_t j = 0; j < height; ++j)
+    for (int32_t i = 0; i < width; ++i) {
+      const double* c = accum + ((size_t)j * width + i) * 3;
+      uint8_t* o = rgb8 + ((size_t)(height - j - 1) * width + i) * 3;
+      for (int k = 0; k < 3; ++k) {
+        double y = std::sqrt(c[k] * inv) * 255.999;  // (x * COLOR_SCALE) as u8, color.rs:31-38
+        o[k] = (std::isnan(y) || y <= 0.0) ? 0 : (y >= 255.0 ? 255 : (uint8_t)y);
+      }
+    }
+  return RT_OK;
+}
+
+}  // extern "C"

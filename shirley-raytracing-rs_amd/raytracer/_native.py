@@ -1,0 +1,187 @@
+"""ctypes mirror of include/shirley_rt.h (render ABI) and include/shirley_host.h (C++ host layer).
+
+The shared libraries are built in-tree by ``make -C shirley-raytracing-rs_amd`` (see
+``__graft_entry__.build``).  There is no fallback: if a library is missing, loading raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_DIR = os.path.join(_PKG_ROOT, "lib")
+BIN_DIR = os.path.join(_PKG_ROOT, "bin")
+
+RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_OOM, RT_E_UNSUPPORTED = 0, 1, 2, 3, 4
+RT_GEOM_SPHERE, RT_GEOM_RECT_XY, RT_GEOM_RECT_YZ, RT_GEOM_RECT_XZ, RT_GEOM_RECT_BOX = range(5)
+RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_LAMBERTIAN, RT_MAT_DIFFUSE_LIGHT, RT_MAT_FAIRY_LIGHT = range(5)
+RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_IMAGE = range(4)
+RT_SKY_ABOVE, RT_SKY_FLAT, RT_SKY_NONE = range(3)
+RT_BVH_REFERENCE, RT_BVH_SAH = 0, 1
+
+_d3 = C.c_double * 3
+_d6 = C.c_double * 6
+
+
+class rt_object(C.Structure):
+    _fields_ = [("geometry", C.c_int32), ("material", C.c_int32), ("p", _d6)]
+
+
+class rt_material(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("texture", C.c_int32), ("albedo", _d3), ("param", C.c_double)]
+
+
+class rt_texture(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("odd", C.c_int32), ("even", C.c_int32), ("table", C.c_int32),
+                ("color", _d3), ("scale", C.c_double)]
+
+
+class rt_perlin_table(C.Structure):
+    _fields_ = [("ranfloat", (C.c_double * 3) * 256), ("perm_x", C.c_int32 * 256),
+                ("perm_y", C.c_int32 * 256), ("perm_z", C.c_int32 * 256)]
+
+
+class rt_image(C.Structure):
+    _fields_ = [("width", C.c_int32), ("height", C.c_int32), ("rgb", C.POINTER(C.c_uint8))]
+
+
+class rt_scene_desc(C.Structure):
+    _fields_ = [("sky", C.c_int32), ("sky_color", _d3),
+                ("n_objects", C.c_int32), ("objects", C.POINTER(rt_object)),
+                ("n_materials", C.c_int32), ("materials", C.POINTER(rt_material)),
+                ("n_textures", C.c_int32), ("textures", C.POINTER(rt_texture)),
+                ("n_perlin", C.c_int32), ("perlin", C.POINTER(rt_perlin_table)),
+                ("n_images", C.c_int32), ("images", C.POINTER(rt_image))]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("image_width", C.c_int32), ("image_height", C.c_int32), ("height", C.c_double),
+                ("width", C.c_double), ("focal_length", C.c_double), ("has_lens", C.c_int32),
+                ("lens_radius", C.c_double), ("origin", _d3), ("w", _d3), ("u", _d3), ("v", _d3),
+                ("focus_length", C.c_double)]
+
+
+class rt_render_params(C.Structure):
+    _fields_ = [("samples", C.c_int32), ("max_depth", C.c_int32), ("seed", C.c_uint64),
+                ("tile_rank", C.c_int32), ("tile_world", C.c_int32), ("sample_chunk", C.c_int32),
+                ("reserved", C.c_int32)]
+
+
+class rt_scene_stats(C.Structure):
+    _fields_ = [("n_objects", C.c_int32), ("n_nodes", C.c_int32), ("n_leaves", C.c_int32),
+                ("depth", C.c_int32), ("device_bytes", C.c_int64)]
+
+
+class rt_counters(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
+                ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double), ("reduce_ms", C.c_double)]
+
+
+class rt_bvh_node(C.Structure):
+    _fields_ = [("box", _d6), ("leaf", C.c_int32), ("lhs", C.c_int32), ("rhs", C.c_int32), ("pad", C.c_int32)]
+
+
+class rt_hit(C.Structure):
+    _fields_ = [("object", C.c_int32), ("front_face", C.c_int32), ("t", C.c_double), ("point", _d3),
+                ("normal", _d3), ("u", C.c_double), ("v", C.c_double)]
+
+
+class sh_camera_spec(C.Structure):
+    _fields_ = [("width", C.c_int32), ("ratio_num", C.c_int32), ("ratio_den", C.c_int32),
+                ("vfov", C.c_double), ("focal_length", C.c_double), ("has_aperture", C.c_int32),
+                ("aperture", C.c_double), ("look_from", _d3), ("look_at", _d3), ("up", _d3),
+                ("override_focus", C.c_int32), ("focus_length", C.c_double)]
+
+
+# every symbol declared in include/shirley_rt.h, with its C signature
+RT_SIGNATURES = {
+    "rt_version": (C.c_char_p, []),
+    "rt_device_count": (C.c_int, [C.POINTER(C.c_int32)]),
+    "rt_create": (C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_destroy": (C.c_int, [C.c_void_p]),
+    "rt_last_error": (C.c_char_p, [C.c_void_p]),
+    "rt_scene_upload": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_desc), C.c_int32]),
+    "rt_scene_stats_get": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_stats)]),
+    "rt_render": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params), C.c_void_p]),
+    "rt_render_scanlines": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params),
+                                      C.c_int32, C.c_int32, C.c_void_p]),
+    "rt_tile_layout": (C.c_int, [C.POINTER(rt_camera), C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "rt_render_device": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params), C.c_void_p,
+                                   C.c_void_p]),
+    "rt_render_tiles_device": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params),
+                                         C.c_void_p, C.c_void_p]),
+    "rt_unpack_tiles_device": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_void_p, C.c_void_p,
+                                         C.c_void_p]),
+    "rt_scene_hit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.POINTER(rt_hit)]),
+    "rt_synchronize": (C.c_int, [C.c_void_p]),
+    "rt_counters_get": (C.c_int, [C.c_void_p, C.POINTER(rt_counters)]),
+    "rt_bvh_build_host": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int32, C.POINTER(C.c_int32),
+                                    C.POINTER(rt_bvh_node), C.POINTER(C.c_int32)]),
+    "rt_tonemap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+}
+
+# every symbol declared in include/shirley_host.h
+SH_SIGNATURES = {
+    "sh_last_error": (C.c_char_p, []),
+    "sh_scene_new": (C.c_void_p, []),
+    "sh_scene_free": (None, [C.c_void_p]),
+    "sh_scene_set_skybox": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_double)]),
+    "sh_scene_add_json": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "sh_scene_len": (C.c_int32, [C.c_void_p]),
+    "sh_scene_to_json": (C.c_int, [C.c_void_p, C.c_int32, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    "sh_scene_from_json": (C.c_int, [C.c_char_p, C.POINTER(C.c_void_p)]),
+    "sh_scene_builtin": (C.c_int, [C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "sh_scene_finalize": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "sh_desc_view": (C.POINTER(rt_scene_desc), [C.c_void_p]),
+    "sh_desc_free": (None, [C.c_void_p]),
+    "sh_camera_build": (C.c_int, [C.POINTER(sh_camera_spec), C.POINTER(rt_camera)]),
+    "sh_default_camera": (C.c_int, [C.c_int32, C.c_char_p, C.c_double, C.c_double, C.c_double,
+                                    C.POINTER(rt_camera)]),
+    "sh_cornell_camera": (C.c_int, [C.c_int32, C.POINTER(rt_camera)]),
+    "sh_scene_camera": (C.c_int, [C.c_char_p, C.c_int32, C.c_char_p, C.c_double, C.c_double, C.c_double,
+                                  C.POINTER(rt_camera)]),
+    "sh_perlin_generate": (C.c_int, [C.c_uint64, C.c_uint32, C.POINTER(rt_perlin_table)]),
+    "sh_write_png": (C.c_int, [C.c_char_p, C.c_void_p, C.c_int32, C.c_int32]),
+    "sh_load_image": (C.c_int, [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                C.POINTER(C.POINTER(C.c_uint8))]),
+    "sh_free": (None, [C.c_void_p]),
+}
+
+_libs: dict = {}
+
+
+def _load(name: str, sigs: dict):
+    if name in _libs:
+        return _libs[name]
+    path = os.path.join(LIB_DIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `make -C {_PKG_ROOT}` "
+                           "(or __graft_entry__.build()); there is no fallback path")
+    lib = C.CDLL(path)
+    for sym, (res, args) in sigs.items():
+        fn = getattr(lib, sym)
+        fn.restype = res
+        fn.argtypes = args
+    _libs[name] = lib
+    return lib
+
+
+def rt_lib():
+    """libshirley_rt.so — the render boundary (HIP kernels)."""
+    return _load("libshirley_rt.so", RT_SIGNATURES)
+
+
+def host_lib():
+    """libshirley_host.so — the C++ host layer (scenes, JSON, camera, PNG)."""
+    return _load("libshirley_host.so", SH_SIGNATURES)
+
+
+class RtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[rt status {code}] {msg}")
+        self.code = code
+
+
+def host_check(code: int):
+    if code != 0:
+        raise RtError(code, host_lib().sh_last_error().decode())

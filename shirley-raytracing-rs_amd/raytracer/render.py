@@ -1,0 +1,154 @@
+"""Render path: the MI355X replacement of render_scene's scanline loop (reference: src/main.rs:65-130,
+src/raytracer/render.rs:17-70), driven through the C ABI of include/shirley_rt.h.
+
+There is no CPU fallback: without a GPU, ``Device()`` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+from .scene import Scene
+
+
+def _check(ctx, code):
+    if code != 0:
+        raise N.RtError(code, N.rt_lib().rt_last_error(ctx).decode())
+
+
+@dataclass
+class RenderSettings:
+    """RenderSettings (argparse.rs:106-123) + the seed/tiling the reference lacks."""
+    samples: int = 100
+    max_reflect: int = 50
+    seed: int = 0x5EED
+    sample_chunk: int = 0
+    tile_rank: int = 0
+    tile_world: int = 1
+
+    def params(self) -> N.rt_render_params:
+        p = N.rt_render_params()
+        p.samples, p.max_depth, p.seed = int(self.samples), int(self.max_reflect), int(self.seed)
+        p.tile_rank, p.tile_world, p.sample_chunk = int(self.tile_rank), int(self.tile_world), int(self.sample_chunk)
+        return p
+
+
+class Device:
+    """One rt_ctx (one MI355X)."""
+
+    def __init__(self, device: int = 0):
+        lib = N.rt_lib()
+        h = C.c_void_p()
+        code = lib.rt_create(int(device), C.byref(h))
+        if code != 0:
+            raise N.RtError(code, f"rt_create(device={device}) failed: no usable HIP device")
+        self._h = h
+        self.scene: Optional[Scene] = None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.rt_lib().rt_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    @property
+    def handle(self):
+        return self._h
+
+    def upload(self, scene: Scene, bvh: str = "reference") -> "Device":
+        builder = {"reference": N.RT_BVH_REFERENCE, "sah": N.RT_BVH_SAH}[bvh]
+        _check(self._h, N.rt_lib().rt_scene_upload(self._h, scene.desc_ptr, builder))
+        self.scene = scene
+        return self
+
+    def stats(self) -> N.rt_scene_stats:
+        s = N.rt_scene_stats()
+        _check(self._h, N.rt_lib().rt_scene_stats_get(self._h, C.byref(s)))
+        return s
+
+    def render(self, camera: N.rt_camera, settings: RenderSettings) -> np.ndarray:
+        """Whole frame -> [H][W][3] f64 per-pixel sums, row 0 = bottom (Image.data layout)."""
+        out = np.zeros((camera.image_height, camera.image_width, 3), dtype=np.float64)
+        p = settings.params()
+        _check(self._h, N.rt_lib().rt_render(self._h, C.byref(camera), C.byref(p), out.ctypes.data))
+        return out
+
+    def render_scanlines(self, camera: N.rt_camera, settings: RenderSettings, line_begin: int,
+                         line_end: int) -> np.ndarray:
+        out = np.zeros((max(0, line_end - line_begin), camera.image_width, 3), dtype=np.float64)
+        p = settings.params()
+        _check(self._h, N.rt_lib().rt_render_scanlines(self._h, C.byref(camera), C.byref(p), line_begin, line_end,
+                                                       out.ctypes.data))
+        return out
+
+    def render_device(self, camera, settings: RenderSettings, accum_ptr: int, stream: int = 0):
+        p = settings.params()
+        _check(self._h, N.rt_lib().rt_render_device(self._h, C.byref(camera), C.byref(p), C.c_void_p(accum_ptr),
+                                                    C.c_void_p(stream or None)))
+
+    def render_tiles_device(self, camera, settings: RenderSettings, packed_ptr: int, stream: int = 0):
+        p = settings.params()
+        _check(self._h, N.rt_lib().rt_render_tiles_device(self._h, C.byref(camera), C.byref(p),
+                                                          C.c_void_p(packed_ptr), C.c_void_p(stream or None)))
+
+    def unpack_tiles_device(self, camera, world: int, gathered_ptr: int, accum_ptr: int, stream: int = 0):
+        _check(self._h, N.rt_lib().rt_unpack_tiles_device(self._h, C.byref(camera), int(world),
+                                                          C.c_void_p(gathered_ptr), C.c_void_p(accum_ptr),
+                                                          C.c_void_p(stream or None)))
+
+    def hit(self, rays: np.ndarray, t_min: float = 0.001, t_max: float = float("inf")):
+        """Closest hits for rays [n][6] (Hittable for Scene, scene/mod.rs:180-190) -> rt_hit array."""
+        r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        out = (N.rt_hit * max(1, len(r)))()
+        _check(self._h, N.rt_lib().rt_scene_hit(self._h, r.ctypes.data, len(r), float(t_min), float(t_max), out))
+        return out[:len(r)]
+
+    def synchronize(self):
+        _check(self._h, N.rt_lib().rt_synchronize(self._h))
+
+    def counters(self) -> N.rt_counters:
+        c = N.rt_counters()
+        _check(self._h, N.rt_lib().rt_counters_get(self._h, C.byref(c)))
+        return c
+
+
+def tile_layout(camera: N.rt_camera, world: int):
+    n, m = C.c_int32(), C.c_int32()
+    code = N.rt_lib().rt_tile_layout(C.byref(camera), int(world), C.byref(n), C.byref(m))
+    if code:
+        raise N.RtError(code, "rt_tile_layout failed")
+    return n.value, m.value
+
+
+def to_image(accum: np.ndarray, samples: int) -> np.ndarray:
+    """image::to_image (image.rs:31-44): [H][W][3] sums -> RGB8 with row 0 = top."""
+    h, w, _ = accum.shape
+    a = np.ascontiguousarray(accum, dtype=np.float64)
+    out = np.zeros((h, w, 3), dtype=np.uint8)
+    code = N.rt_lib().rt_tonemap(a.ctypes.data, w, h, int(samples), out.ctypes.data)
+    if code:
+        raise N.RtError(code, "rt_tonemap failed")
+    return out
+
+
+def write_png(path: str, rgb8: np.ndarray):
+    a = np.ascontiguousarray(rgb8, dtype=np.uint8)
+    N.host_check(N.host_lib().sh_write_png(path.encode(), a.ctypes.data, a.shape[1], a.shape[0]))
+
+
+def render_scene(settings: RenderSettings, scene: Scene, camera: N.rt_camera, output: Optional[str] = None,
+                 device: Optional[Device] = None, bvh: str = "reference") -> np.ndarray:
+    """render_scene (main.rs:65-130): samples 0 -> 1, render, to_image + PNG when ``output`` is set."""
+    if settings.samples == 0:
+        settings = RenderSettings(**{**settings.__dict__, "samples": 1})
+    dev = device or Device(0)
+    dev.upload(scene, bvh)
+    accum = dev.render(camera, settings)
+    if output:
+        write_png(output, to_image(accum, settings.samples))
+    return accum

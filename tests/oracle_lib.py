@@ -1,0 +1,164 @@
+"""ctypes binding of oracle/liboracle.so — the CPU parity checker (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "shirley-raytracing-rs_amd"))
+from raytracer import _native as N  # noqa: E402
+
+ORACLE_DIR = os.path.join(REPO, "oracle")
+ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+
+_d6 = C.c_double * 6
+
+
+class or_counters(C.Structure):
+    _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
+                ("prim_tests", C.c_uint64)]
+
+
+class or_hit(C.Structure):
+    _fields_ = [("hit", C.c_int32), ("object", C.c_int32), ("t", C.c_double), ("point", C.c_double * 3),
+                ("normal", C.c_double * 3), ("front_face", C.c_int32), ("u", C.c_double), ("v", C.c_double)]
+
+
+_SIGS = {
+    "or_philox4x32_10": (None, [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
+    "or_rng_u64": (C.c_uint64, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "or_rng_f64": (C.c_double, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "or_fmin": (C.c_double, [C.c_double, C.c_double]),
+    "or_fmax": (C.c_double, [C.c_double, C.c_double]),
+    "or_non_nan": (C.c_double, [C.c_double, C.c_double]),
+    "or_aabb_hit": (C.c_int32, [_d6, _d6, C.c_double, C.c_double]),
+    "or_aabb_hit2": (C.c_int32, [_d6, _d6, C.c_double, C.c_double]),
+    "or_surrounding_box": (None, [_d6, _d6, _d6]),
+    "or_aabb_area": (C.c_double, [_d6]),
+    "or_object_bbox": (C.c_int32, [C.POINTER(N.rt_object), _d6]),
+    "or_object_hit": (C.c_int32, [C.POINTER(N.rt_object), _d6, C.c_double, C.c_double, C.POINTER(or_hit)]),
+    "or_scene_new": (C.c_void_p, [C.POINTER(N.rt_scene_desc)]),
+    "or_scene_free": (None, [C.c_void_p]),
+    "or_tree_size": (C.c_int32, [C.c_void_p]),
+    "or_tree_root": (C.c_int32, [C.c_void_p]),
+    "or_tree_node": (None, [C.c_void_p, C.c_int32, _d6, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                            C.POINTER(C.c_int32)]),
+    "or_scene_hit": (None, [C.c_void_p, _d6, C.c_double, C.c_double, C.POINTER(or_hit)]),
+    "or_texture_value": (None, [C.c_void_p, C.c_int32, C.c_double, C.c_double, C.POINTER(C.c_double),
+                                C.POINTER(C.c_double)]),
+    "or_perlin_noise": (C.c_double, [C.c_void_p, C.c_int32, C.POINTER(C.c_double)]),
+    "or_perlin_turbulence": (C.c_double, [C.c_void_p, C.c_int32, C.POINTER(C.c_double), C.c_int32]),
+    "or_pixel_ray": (None, [C.POINTER(N.rt_camera), C.c_uint64, C.c_int32, C.c_int32, C.c_uint32, _d6]),
+    "or_sample_color": (None, [C.c_void_p, C.POINTER(N.rt_camera), C.POINTER(N.rt_render_params), C.c_int32,
+                               C.c_int32, C.c_uint32, C.POINTER(C.c_double), C.POINTER(or_counters)]),
+    "or_render_scanline": (None, [C.c_void_p, C.POINTER(N.rt_camera), C.POINTER(N.rt_render_params), C.c_int32,
+                                  C.c_void_p, C.POINTER(or_counters)]),
+    "or_render_rows": (C.c_int32, [C.c_void_p, C.POINTER(N.rt_camera), C.POINTER(N.rt_render_params), C.c_int32,
+                                   C.c_int32, C.c_int32, C.c_void_p, C.POINTER(or_counters)]),
+    "or_tonemap": (None, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(ORACLE_DIR, "oracle.c")
+        if not os.path.exists(ORACLE_SO) or os.path.getmtime(ORACLE_SO) < os.path.getmtime(src):
+            subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
+        _lib = C.CDLL(ORACLE_SO)
+        for sym, (res, args) in _SIGS.items():
+            fn = getattr(_lib, sym)
+            fn.restype, fn.argtypes = res, args
+    return _lib
+
+
+def d6(v):
+    return _d6(*[float(x) for x in v])
+
+
+class OracleScene:
+    """or_scene: SceneBuilder::finalize restated (BVH by the reference's split rules)."""
+
+    def __init__(self, desc):
+        self.keep = desc  # keep the arrays behind the desc alive
+        d = desc.desc if hasattr(desc, "desc") else desc
+        self.h = lib().or_scene_new(C.byref(d))
+        if not self.h:
+            raise RuntimeError("or_scene_new failed")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().or_scene_free(self.h)
+            self.h = None
+
+    def hit(self, ray, t_min=0.001, t_max=float("inf")):
+        out = or_hit()
+        lib().or_scene_hit(self.h, d6(ray), t_min, t_max, C.byref(out))
+        return out
+
+    def tree(self):
+        n = lib().or_tree_size(self.h)
+        nodes = []
+        for i in range(n):
+            b = _d6()
+            leaf, lhs, rhs = C.c_int32(), C.c_int32(), C.c_int32()
+            lib().or_tree_node(self.h, i, b, C.byref(leaf), C.byref(lhs), C.byref(rhs))
+            nodes.append((tuple(b), leaf.value, lhs.value, rhs.value))
+        return nodes, lib().or_tree_root(self.h)
+
+    def render(self, cam, params, line_begin=0, line_end=None, threads=None):
+        line_end = cam.image_height if line_end is None else line_end
+        out = np.zeros((line_end - line_begin, cam.image_width, 3), dtype=np.float64)
+        cnt = or_counters()
+        threads = threads or min(8, os.cpu_count() or 1)
+        rc = lib().or_render_rows(self.h, C.byref(cam), C.byref(params), line_begin, line_end, threads,
+                                  out.ctypes.data, C.byref(cnt))
+        if rc:
+            raise RuntimeError("or_render_rows failed")
+        return out, cnt
+
+    def sample(self, cam, params, px, py, s):
+        out = (C.c_double * 3)()
+        cnt = or_counters()
+        lib().or_sample_color(self.h, C.byref(cam), C.byref(params), px, py, s, out, C.byref(cnt))
+        return np.array(out[:]), cnt
+
+
+class SphereScene:
+    """An rt_scene_desc of bare spheres (one Lambertian grey material), built with ctypes only —
+    the shape of the reference's bbox_tree.rs unit tests (BboxTree<Sphere>)."""
+
+    def __init__(self, spheres, sky=N.RT_SKY_ABOVE):
+        n = len(spheres)
+        self.objs = (N.rt_object * max(1, n))()
+        for i, (c, r) in enumerate(spheres):
+            self.objs[i].geometry = N.RT_GEOM_SPHERE
+            self.objs[i].material = 0
+            self.objs[i].p[:] = [c[0], c[1], c[2], r, 0.0, 0.0]
+        self.mats = (N.rt_material * 1)()
+        self.mats[0].kind, self.mats[0].texture = N.RT_MAT_LAMBERTIAN, 0
+        self.texs = (N.rt_texture * 1)()
+        self.texs[0].kind = N.RT_TEX_SOLID
+        self.texs[0].color[:] = [0.5, 0.5, 0.5]
+        self.desc = N.rt_scene_desc()
+        self.desc.sky = sky
+        self.desc.n_objects, self.desc.objects = n, self.objs
+        self.desc.n_materials, self.desc.materials = 1, self.mats
+        self.desc.n_textures, self.desc.textures = 1, self.texs
+        self.desc_ptr = C.pointer(self.desc)
+
+
+def params(samples, max_depth=50, seed=0x5EED, chunk=0, rank=0, world=1):
+    p = N.rt_render_params()
+    p.samples, p.max_depth, p.seed = samples, max_depth, seed
+    p.sample_chunk, p.tile_rank, p.tile_world = chunk, rank, world
+    return p
