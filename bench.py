@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--scene", default="random")
     ap.add_argument("--bvh", default="sah", choices=["reference", "sah"])
     ap.add_argument("--sample-chunk", type=int, default=0)
-    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
@@ -52,13 +52,18 @@ def cpu_baseline(scene, cam, args):
     import oracle_lib as O
     osc = O.OracleScene(scene)
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    p = O.params(args.cpu_spp, args.max_depth, args.seed)
+    # calibrate on one sample per pixel, then size the measured sample to ~cpu_seconds of wall time
     t0 = time.perf_counter()
-    _, cnt = osc.render(cam, p, threads=threads)
+    osc.render(cam, O.params(1, args.max_depth, args.seed + 1), threads=threads)
+    per_spp = time.perf_counter() - t0
+    spp = int(max(1, min(args.spp, round(args.cpu_seconds / max(per_spp, 1e-3)))))
+    t0 = time.perf_counter()
+    _, cnt = osc.render(cam, O.params(spp, args.max_depth, args.seed), threads=threads)
     dt = time.perf_counter() - t0
     return {"value": round(cnt.samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{args.scene} {cam.image_width}x{cam.image_height} @ {args.cpu_spp} spp "
-                      f"({cnt.samples} samples, {dt:.1f} s wall on {threads} threads; f64 C oracle)"}
+            "sample": f"{args.scene} {cam.image_width}x{cam.image_height} @ {spp} spp (full frame, reduced spp; "
+                      f"{cnt.samples} samples, {dt:.1f} s wall on {threads} threads; f64 C oracle restating "
+                      f"the reference path, -O2)"}
 
 
 def main():

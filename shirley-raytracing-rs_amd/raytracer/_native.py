@@ -166,8 +166,23 @@ def _load(name: str, sigs: dict):
     return lib
 
 
+def _single_hip_runtime():
+    """PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7, but NEEDED as
+    "libamdhip64.so"): if libshirley_rt.so pulled /opt/rocm's copy in first, a later torch import
+    would load a second HIP/HSA runtime that finds no GPU.  Importing torch first makes our NEEDED
+    libamdhip64.so.7 resolve to the runtime already in the process: one runtime, shared streams."""
+    if os.environ.get("SHIRLEY_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def rt_lib():
     """libshirley_rt.so — the render boundary (HIP kernels)."""
+    if "libshirley_rt.so" not in _libs:
+        _single_hip_runtime()
     return _load("libshirley_rt.so", RT_SIGNATURES)
 
 

@@ -2,12 +2,13 @@
 
 Tolerance (north star: "within a stated per-channel float tolerance under a fixed RNG seed"):
 both sides evaluate the reference's binary64 formulas in the same order with the same counter RNG,
-so a pixel's per-sample colours are bit-identical unless a libm/ocml transcendental (acos, atan2,
-sin, pow) differs by an ulp AND that flips a comparison (checker sign, Schlick vs U, texel index),
-or two objects tie at exactly the same t.  The test therefore demands
-  * >= 99.9 % of pixel channels bit-identical (sample_chunk = spp: in-order sums like render.rs:58-69),
-  * every channel within PIXEL_TOL = 1e-9 * spp absolute of the oracle, except at most 0.1 % of
-    pixels (a flipped path changes one sample by at most max-radiance).
+so per-sample colours agree to the last ulp except where the device's transcendentals (ocml sin,
+acos, atan2, pow) differ from glibc's by an ulp — a last-bit difference in an attenuation — or,
+rarely, such an ulp flips a comparison (checker sign, Schlick vs U, texel index) or two objects tie
+at exactly the same t, which changes one whole path.  The test therefore demands
+  * >= 95 % of pixel channels bit-identical (sample_chunk = spp: in-order sums like render.rs:58-69),
+  * every channel within TOL = 1e-10 * spp absolute of the oracle, except at most 0.1 % of pixels
+    (a flipped path changes one sample by up to the path's radiance).
 """
 import ctypes as C
 
@@ -22,12 +23,12 @@ pytestmark = pytest.mark.gpu
 SEED = 0x5EED
 
 
-def check_parity(gpu_img, ora_img, spp, frac_exact=0.999, frac_outlier=0.001):
+def check_parity(gpu_img, ora_img, spp, frac_exact=0.95, frac_outlier=0.001):
     assert gpu_img.shape == ora_img.shape
     assert np.isfinite(gpu_img).all() == np.isfinite(ora_img).all()
     exact = np.mean(gpu_img == ora_img)
     diff = np.abs(gpu_img - ora_img)
-    bad_px = np.any(diff > 1e-9 * spp, axis=-1)
+    bad_px = np.any(diff > 1e-10 * spp, axis=-1)
     assert exact >= frac_exact, f"only {exact:.5f} of channels bit-identical (max diff {diff.max():.3g})"
     assert bad_px.mean() <= frac_outlier, f"{bad_px.sum()} pixels outside tolerance"
 
@@ -120,9 +121,10 @@ def test_scanlines_equal_full_frame(gpu):
     assert np.array_equal(part, full[5:17])
     row = np.zeros((cam.image_width, 3))
     cnt = O.or_counters()
-    O.lib().or_render_scanline(O.OracleScene(scene).h, C.byref(cam), C.byref(O.params(spp, 50, SEED)), 9,
-                               row.ctypes.data, C.byref(cnt))
-    check_parity(part[4:5], row[None], spp, frac_exact=0.99, frac_outlier=0.05)
+    osc = O.OracleScene(scene)
+    O.lib().or_render_scanline(osc.h, C.byref(cam), C.byref(O.params(spp, 50, SEED)), 9, row.ctypes.data,
+                               C.byref(cnt))
+    check_parity(part[4:5], row[None], spp, frac_exact=0.9, frac_outlier=0.05)
 
 
 def test_tiles_gather_unpack_equals_full_frame(gpu):
