@@ -93,14 +93,14 @@ def main():
     if world > 1:
         n_tiles, max_tiles = rt.tile_layout(cam, world)
         packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
-        gathered = torch.zeros((world, max_tiles, 64, 3), dtype=torch.float64, device="cuda")
+        from raytracer.parallel import gather_tiles
 
     def step():
         if world == 1:
             dev.render_device(cam, settings, accum.data_ptr(), sh)
         else:
             dev.render_tiles_device(cam, settings, packed.data_ptr(), sh)
-            dist.all_gather_into_tensor(gathered, packed)  # RCCL over xGMI; rank 0 assembles the frame
+            gathered = gather_tiles(packed, world)  # RCCL all-gather over xGMI; rank 0 assembles the frame
             if rank == 0:
                 dev.unpack_tiles_device(cam, world, gathered.data_ptr(), accum.data_ptr(), sh)
 

@@ -1,0 +1,58 @@
+"""Multi-GPU frame sharding: interleaved 8x8 tiles per rank + one gather.
+
+tile k of the frame (row-major over the tile grid) belongs to rank k % world; a rank's packed buffer
+holds its tiles in order, [max_tiles][64][3] f64, lane l of a tile = pixel (8*tx + l%8, 8*ty + l//8).
+The device kernels (rt_render_tiles_device / rt_unpack_tiles_device) and the numpy mirror below use
+the same mapping.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+TILE = 8
+
+
+def tile_grid(width: int, height: int):
+    return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
+
+
+def max_tiles_per_rank(width: int, height: int, world: int) -> int:
+    tx, ty = tile_grid(width, height)
+    return (tx * ty + world - 1) // world
+
+
+def rank_slots(width: int, height: int, rank: int, world: int):
+    """(py, px, valid) for every packed slot of `rank` ([max_tiles*64] each)."""
+    tx, ty = tile_grid(width, height)
+    m = max_tiles_per_rank(width, height, world)
+    lt = np.repeat(np.arange(m), TILE * TILE)
+    lp = np.tile(np.arange(TILE * TILE), m)
+    gt = lt * world + rank
+    px = (gt % tx) * TILE + lp % TILE
+    py = (gt // tx) * TILE + lp // TILE
+    valid = (gt < tx * ty) & (px < width) & (py < height)
+    return py, px, valid
+
+
+def unpack_host(gathered: np.ndarray, width: int, height: int, world: int) -> np.ndarray:
+    """numpy mirror of unpack_kernel: [world][max_tiles][64][3] -> [H][W][3]."""
+    out = np.zeros((height, width, 3), dtype=np.float64)
+    g = gathered.reshape(world, -1, 3)
+    for r in range(world):
+        py, px, valid = rank_slots(width, height, r, world)
+        out[py[valid], px[valid]] = g[r][valid]
+    return out
+
+
+def gather_tiles(packed, world: int):
+    """All ranks' packed tile buffers -> [world, ...] on every rank (RCCL all_gather over xGMI for
+    CUDA tensors; gloo for CPU tensors in the tests)."""
+    import torch
+    import torch.distributed as dist
+    if packed.is_cuda:
+        out = torch.empty((world,) + tuple(packed.shape), dtype=packed.dtype, device=packed.device)
+        dist.all_gather_into_tensor(out, packed.contiguous())
+        return out
+    parts = [torch.empty_like(packed) for _ in range(world)]
+    dist.all_gather(parts, packed.contiguous())
+    return torch.stack(parts)
