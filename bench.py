@@ -39,6 +39,9 @@ def parse():
     ap.add_argument("--scene", default="random")
     ap.add_argument("--bvh", default="sah", choices=["reference", "sah"])
     ap.add_argument("--sample-chunk", type=int, default=0)
+    ap.add_argument("--nodes", default="auto", choices=["auto", "global", "half-lds", "lds"], help="BVH node placement")
+    ap.add_argument("--engine", default="auto", choices=["auto", "megakernel", "wavefront"])
+    ap.add_argument("--timing", action="store_true", help="per-launch HIP-event timing of the wavefront kernels")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
@@ -84,9 +87,10 @@ def main():
     cam = rt.scene_camera(args.scene, args.width, args.aspect)
     W, H = cam.image_width, cam.image_height
     dev = rt.Device(local)
-    dev.upload(scene, args.bvh)
+    dev.upload(scene, args.bvh, args.nodes)
     settings = rt.RenderSettings(samples=args.spp, max_reflect=args.max_depth, seed=args.seed,
-                                 sample_chunk=args.sample_chunk, tile_rank=rank, tile_world=world)
+                                 sample_chunk=args.sample_chunk, tile_rank=rank, tile_world=world,
+                                 engine=args.engine, timing=args.timing)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
@@ -110,13 +114,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, segments = [], []
+    kernel_ms, segments, laps = [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
         kernel_ms.append(c.kernel_ms)
         segments.append(c.segments)
+        laps.append((c.engine, c.iterations, c.slots, c.extend_ms, c.shade_ms, c.texture_ms))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -149,6 +154,10 @@ def main():
         "config": {"workload": f"{args.scene} {W}x{H} @ {args.spp}spp, max_depth {args.max_depth}, seed "
                                f"{args.seed:#x}", "scene": args.scene, "width": W, "height": H, "spp": args.spp,
                    "max_depth": args.max_depth, "bvh": args.bvh, "parallelism": f"tiles8x8/{world}",
+                   "engine": {1: "megakernel", 2: "wavefront"}.get(laps[-1][0]), "rounds": laps[-1][1],
+                   "slots": laps[-1][2],
+                   "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
+                                       "texture": round(laps[-1][5], 3)} if args.timing else None,
                    "segments_per_sample": round(seg / (W * H * args.spp / world), 4) if world == 1 else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

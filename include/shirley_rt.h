@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1
+#define RT_ABI_VERSION 2
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -48,7 +48,20 @@ enum { RT_SKY_ABOVE = 0, RT_SKY_FLAT = 1, RT_SKY_NONE = 2 };
 /* BVH builder selection for rt_scene_upload */
 enum {
   RT_BVH_REFERENCE = 0, /* bvh/bbox_tree/constructor.rs split rules (median/midpoint on min-x/y/z, volume score) */
-  RT_BVH_SAH = 1        /* binned surface-area heuristic (performance option; same hits up to measure-zero ties) */
+  RT_BVH_SAH = 1,       /* binned surface-area heuristic (performance option; same hits up to measure-zero ties) */
+  /* node placement flags OR-ed into the builder argument (testing / tuning) */
+  RT_BVH_NODES_GLOBAL = 0x100,   /* every node read through L1/L2 (the default) */
+  RT_BVH_NODES_HALF_LDS = 0x200, /* top half of the nodes copied into LDS per block (mixed path) */
+  RT_BVH_NODES_LDS = 0x400       /* as many nodes in LDS as fit next to the traversal stacks */
+};
+/* Trace engine for rt_render_params.engine.  Both compute the same ray_color() arithmetic and give
+ * the same pixels; they differ only in how the bounce loop is scheduled on the GPU. */
+enum {
+  RT_ENGINE_AUTO = 0,       /* the faster engine on MI355X (today: the megakernel; env SHIRLEY_ENGINE overrides) */
+  RT_ENGINE_MEGAKERNEL = 1, /* one persistent kernel runs whole paths, lane-level path regeneration */
+  RT_ENGINE_WAVEFRONT = 2,  /* extend / shade / texture kernels over a pool of path slots in HBM;
+                             * the host loop blocks until the frame is traced */
+  RT_ENGINE_TIMING = 0x10   /* flag: time every kernel launch with HIP events (rt_counters *_ms) */
 };
 
 /* One scene object = SceneLoadObject{geometry, material} (scene/mod.rs:23-27). */
@@ -133,7 +146,7 @@ typedef struct rt_render_params {
   int32_t tile_rank;    /* interleaved 8x8-tile sharding: this call renders tiles k with k % tile_world == tile_rank */
   int32_t tile_world;   /* 1 = whole frame */
   int32_t sample_chunk; /* samples per work unit (0 = automatic; >= samples gives in-order per-pixel sums) */
-  int32_t reserved;
+  int32_t engine;       /* RT_ENGINE_* (0 = automatic), optionally | RT_ENGINE_TIMING */
 } rt_render_params;
 
 typedef struct rt_scene_stats {
@@ -150,8 +163,14 @@ typedef struct rt_counters {
   uint64_t segments;    /* ray_color loop iterations that traced a ray (hit + miss) */
   uint64_t node_visits; /* BVH child-box tests */
   uint64_t prim_tests;  /* primitive intersection calls */
-  double kernel_ms;     /* device time of the trace kernel (HIP events) */
+  double kernel_ms;     /* device time of the trace (all trace kernels of the frame, HIP events) */
   double reduce_ms;     /* device time of the partial-sum reduce kernel */
+  int32_t engine;       /* RT_ENGINE_MEGAKERNEL or RT_ENGINE_WAVEFRONT: the engine that ran */
+  int32_t iterations;   /* wavefront: extend/shade/texture rounds (0 for the megakernel) */
+  uint64_t slots;       /* wavefront: path slots in flight */
+  double extend_ms;     /* wavefront + RT_ENGINE_TIMING: summed device time of wf_extend launches */
+  double shade_ms;      /* ... wf_shade launches */
+  double texture_ms;    /* ... wf_texture launches */
 } rt_counters;
 
 typedef struct rt_ctx rt_ctx;

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -17,8 +18,8 @@
 #include "rt_layout.h"
 
 namespace rt {
-size_t trace_lds_bytes(int stack_depth);
-hipError_t trace_occupancy(int stack_depth, int* blocks_per_cu);
+size_t trace_lds_bytes(int n_lds_nodes, int stack_depth);
+hipError_t trace_occupancy(const DScene& S, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
                          int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
@@ -26,6 +27,15 @@ hipError_t launch_unpack(const double* gathered, int world, int max_tiles, int n
                          int height, double* out, hipStream_t stream);
 hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, double t_max, void* out,
                       hipStream_t stream);
+// wavefront.hip
+size_t wf_extend_lds(int n_lds_nodes, int stack_depth);
+int wf_extend_threads();
+int wf_grid_threads();
+hipError_t wf_prepare(const DScene& S, int* extend_blocks_per_cu);
+hipError_t wf_start(const WfParams& P, int grid_blocks, hipStream_t s);
+hipError_t wf_launch_extend(const WfParams& P, int extend_blocks, hipStream_t s);
+hipError_t wf_launch_shade(const WfParams& P, int grid_blocks, hipStream_t s);
+hipError_t wf_launch_texture(const WfParams& P, int grid_blocks, hipStream_t s);
 }  // namespace rt
 
 using namespace rt;
@@ -46,10 +56,21 @@ struct rt_ctx {
   DevBuf nodes, prims, mats, texs, perlin, images, texels;
   rt_scene_stats stats{};
   int blocks_per_cu = 0;
+  // wavefront engine: the scene with its LDS node count sized for the extend block
+  DScene wf_scene{};
+  int wf_blocks_per_cu = 0;
+  bool has_perlin = false;
   // per-render scratch
   DevBuf partial, accum, counters, unit_counter;
+  DevBuf wf_pool, wf_iters;          // path slots (SoA) + texture queue; per-iteration counters ring
+  uint32_t* wf_host = nullptr;       // pinned readback of the retired-slot count, one word per batch
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t wf_ev[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> lap_ev;    // RT_ENGINE_TIMING: one event after every launch
   bool have_timing = false;
+  int last_engine = 0, last_iters = 0, last_timing = 0;
+  uint64_t last_slots = 0;
+  double lap_ms[3] = {0, 0, 0};
 };
 
 namespace {
@@ -193,40 +214,42 @@ void box_to6(const Box& b, double* o) {
   }
 }
 
-// BuiltTree -> DNode array in depth-first order: node 0 = top node whose child 0 is the root.
+// f64 -> f32 rounded toward -inf / +inf
+void box_to_node(const Box& b, double* o) {
+  for (int k = 0; k < 3; ++k) {
+    o[k] = b.mn[k];
+    o[k + 3] = b.mx[k];
+  }
+}
+
+// BuiltTree -> DNode array in breadth-first order (node 0 = top node whose child 0 is the root), so
+// that a prefix of the array = the top levels of the tree, which the kernels keep in LDS.
 void flatten(const BuiltTree& t, std::vector<DNode>& out) {
   out.clear();
   DNode top{};
   top.child[0] = kEmptyChild;
   top.child[1] = kEmptyChild;
-  for (int k = 0; k < 6; ++k) top.box[1][k] = (k < 3) ? INFINITY : -INFINITY;
   out.push_back(top);
-  if (t.root < 0) {
-    for (int k = 0; k < 6; ++k) out[0].box[0][k] = (k < 3) ? INFINITY : -INFINITY;
-    return;
-  }
-  // child reference for a BuiltTree node: ~object for a leaf, else the DNode index (assigned on visit)
+  if (t.root < 0) return;
   struct Item {
     int32_t built;
     int32_t parent;
     int slot;
   };
-  std::vector<Item> st{{t.root, 0, 0}};
-  while (!st.empty()) {
-    Item it = st.back();
-    st.pop_back();
+  std::vector<Item> q{{t.root, 0, 0}};
+  for (size_t head = 0; head < q.size(); ++head) {
+    Item it = q[head];
     const BuildNode& bn = t.nodes[it.built];
-    box_to6(bn.box, out[it.parent].box[it.slot]);
+    box_to_node(bn.box, out[it.parent].box[it.slot]);
     if (bn.leaf >= 0) {
       out[it.parent].child[it.slot] = ~bn.leaf;
       continue;
     }
     int32_t idx = (int32_t)out.size();
     out[it.parent].child[it.slot] = idx;
-    DNode n{};
-    out.push_back(n);
-    st.push_back({bn.rhs, idx, 1});
-    st.push_back({bn.lhs, idx, 0});
+    out.push_back(DNode{});
+    q.push_back({bn.lhs, idx, 0});
+    q.push_back({bn.rhs, idx, 1});
   }
 }
 
@@ -281,6 +304,170 @@ int check_render_args(rt_ctx* c, const rt_camera* cam, const rt_render_params* p
   return RT_OK;
 }
 
+constexpr int kWfDefaultChunk = 8;
+constexpr long long kWfDefaultSlots = 1LL << 21;
+constexpr int kWfBatch = 32;  // iterations launched between two host checks of the termination flag
+
+int default_engine() {
+  const char* e = getenv("SHIRLEY_ENGINE");
+  if (e && !strcmp(e, "megakernel")) return RT_ENGINE_MEGAKERNEL;
+  if (e && !strcmp(e, "wavefront")) return RT_ENGINE_WAVEFRONT;
+  return RT_ENGINE_MEGAKERNEL;  // measured faster on MI355X
+}
+
+// Carve the slot arrays out of one allocation (each array 256-B aligned).
+struct Carver {
+  char* base;
+  size_t off = 0;
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base + off);
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+size_t wf_pool_bytes(size_t n) {
+  Carver cv{nullptr};
+  for (int i = 0; i < 17; ++i) cv.take<double>(n);  // 15 path doubles + ht + tq.px/py/pz/scale below
+  cv.take<uint64_t>(n);
+  for (int i = 0; i < 11; ++i) cv.take<uint32_t>(n);
+  cv.take<uint8_t>(n);
+  for (int i = 0; i < 3; ++i) cv.take<double>(n);
+  for (int i = 0; i < 3; ++i) cv.take<int32_t>(n);
+  cv.take<unsigned long long>(2 * (n / kWave));  // unit windows
+  cv.take<uint32_t>(n / kWave);                  // texture queue counts
+  cv.take<unsigned>(64);                         // retired counter
+  return cv.off + 256;
+}
+
+void wf_carve(void* base, size_t n, WfParams& P) {
+  WfState& st = P.st;
+  WfTexQ& tq = P.tq;
+  Carver cv{static_cast<char*>(base)};
+  double** dp[] = {&st.ox, &st.oy, &st.oz, &st.dx, &st.dy, &st.dz, &st.ax, &st.ay, &st.az,
+                   &st.ex, &st.ey, &st.ez, &st.sx, &st.sy, &st.sz, &st.ht, &tq.px};
+  for (double** q : dp) *q = cv.take<double>(n);
+  st.part = cv.take<uint64_t>(n);
+  st.pixel = cv.take<uint32_t>(n);
+  st.sample = cv.take<uint32_t>(n);
+  st.draw = cv.take<uint32_t>(n);
+  st.c2 = cv.take<uint32_t>(n);
+  st.c3 = cv.take<uint32_t>(n);
+  st.s_next = cv.take<int32_t>(n);
+  st.s_end = cv.take<int32_t>(n);
+  st.depth = cv.take<int32_t>(n);
+  st.hprim = cv.take<int32_t>(n);
+  st.hface = cv.take<int32_t>(n);
+  (void)cv.take<uint32_t>(n);  // spare
+  st.state = cv.take<uint8_t>(n);
+  tq.py = cv.take<double>(n);
+  tq.pz = cv.take<double>(n);
+  tq.scale = cv.take<double>(n);
+  tq.slot = cv.take<int32_t>(n);
+  tq.tex = cv.take<int32_t>(n);
+  tq.kind = cv.take<int32_t>(n);
+  P.win = cv.take<unsigned long long>(2 * (n / kWave));
+  tq.count = cv.take<uint32_t>(n / kWave);
+  P.retired = cv.take<unsigned>(64);
+}
+
+// The wavefront engine: start (every slot takes a unit and a camera ray), then rounds of
+// extend -> shade -> texture until no slot holds work.  Rounds are launched in batches; the host
+// reads the retired-slot count after the previous batch while the next batch runs, so the GPU
+// never waits on the host.
+int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
+  const uint64_t n_units = kp.work.n_units;
+  long long slots = kWfDefaultSlots;
+  if (const char* e = getenv("SHIRLEY_WF_SLOTS")) slots = std::max(64LL, atoll(e));
+  slots = std::min<long long>(slots, std::max<long long>(64, (long long)n_units));
+  slots = (slots + 63) / 64 * 64;
+  const size_t n = (size_t)slots;
+  int st = ensure(c, c->wf_pool, wf_pool_bytes(n));
+  if (st) return st;
+  st = ensure(c, c->wf_iters, sizeof(WfIter));  // extend cursors (wf_shade re-zeroes them each round)
+  if (st) return st;
+
+  WfParams P{};
+  P.scene = c->wf_scene;
+  P.cam = kp.cam;
+  P.work = kp.work;
+  wf_carve(c->wf_pool.p, n, P);
+  P.n_slots = (uint32_t)n;
+  P.partial = kp.partial;
+  P.unit_counter = kp.unit_counter;
+  P.counters = kp.counters;
+  P.it = static_cast<WfIter*>(c->wf_iters.p);
+
+  HIP_TRY(c, hipMemsetAsync(P.st.state, 0, n, s));           // kSlotIdle
+  HIP_TRY(c, hipMemsetAsync(P.st.pixel, 0xff, n * 4, s));    // no unit
+  HIP_TRY(c, hipMemsetAsync(P.it, 0, sizeof(WfIter), s));
+  HIP_TRY(c, hipMemsetAsync(P.retired, 0, sizeof(unsigned), s));
+  const int gt = wf_grid_threads();
+  const int grid = (int)((n + gt - 1) / gt);
+  const bool texture_pass = c->has_perlin;  // deferred entries exist only for Perlin leaves
+  const int ext_blocks = std::max(1, c->cu_count * std::max(1, c->wf_blocks_per_cu));
+
+  // timing: an event before and after each launch of a round, elapsed times summed per kernel
+  std::vector<hipEvent_t>& lap = c->lap_ev;
+  std::vector<int> lap_tag;  // kernel the interval starting at this mark belongs to (3: none)
+  auto lap_mark = [&](int tag) -> int {
+    if (!timing) return RT_OK;
+    if (lap_tag.size() == lap.size()) {
+      hipEvent_t e;
+      HIP_TRY(c, hipEventCreate(&e));
+      lap.push_back(e);
+    }
+    HIP_TRY(c, hipEventRecord(lap[lap_tag.size()], s));
+    lap_tag.push_back(tag);
+    return RT_OK;
+  };
+
+  HIP_TRY(c, hipEventRecord(c->ev[0], s));
+  HIP_TRY(c, wf_start(P, grid, s));
+  long long iter = 1;
+  // safety bound: every round advances each working slot by one segment or one regeneration
+  const long long max_iters = 64 + 2LL * ((long long)((n_units + n - 1) / n) + 1) *
+                                       (long long)(kp.work.chunk) * (long long)(kp.work.max_depth + 2);
+  int batch = 0;
+  for (;;) {
+    for (int k = 0; k < kWfBatch; ++k, ++iter) {
+      if ((st = lap_mark(0))) return st;
+      HIP_TRY(c, wf_launch_extend(P, ext_blocks, s));
+      if ((st = lap_mark(1))) return st;
+      HIP_TRY(c, wf_launch_shade(P, grid, s));
+      if ((st = lap_mark(2))) return st;
+      if (texture_pass) HIP_TRY(c, wf_launch_texture(P, grid, s));
+      if ((st = lap_mark(3))) return st;
+    }
+    HIP_TRY(c, hipMemcpyAsync(&c->wf_host[batch & 1], P.retired, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipEventRecord(c->wf_ev[batch & 1], s));
+    if (batch > 0) {
+      HIP_TRY(c, hipEventSynchronize(c->wf_ev[(batch - 1) & 1]));
+      if (c->wf_host[(batch - 1) & 1] >= (uint32_t)n) break;  // every slot retired
+    }
+    ++batch;
+    if (iter > max_iters) return fail(c, RT_E_HIP, "wavefront engine did not terminate after %lld rounds", iter);
+  }
+  HIP_TRY(c, hipEventRecord(c->ev[1], s));
+  c->last_iters = (int)iter;
+  c->last_slots = n;
+  c->last_timing = timing;
+  if (timing && !lap_tag.empty()) {
+    HIP_TRY(c, hipEventSynchronize(lap[lap_tag.size() - 1]));
+    double acc[3] = {0, 0, 0};
+    for (size_t i = 0; i + 1 < lap_tag.size(); ++i) {
+      if (lap_tag[i] > 2) continue;
+      float ms = 0.f;
+      HIP_TRY(c, hipEventElapsedTime(&ms, lap[i], lap[i + 1]));
+      acc[lap_tag[i]] += ms;
+    }
+    for (int k = 0; k < 3; ++k) c->lap_ms[k] = acc[k];
+  }
+  return RT_OK;
+}
+
 // trace + reduce for tile rows [ty0, ty1) ; out layout: packed tiles (packed=1) or rows [row0,row1)
 int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int ty0, int ty1, int row0, int row1,
                   int packed, double* out_dev, hipStream_t s) {
@@ -291,10 +478,18 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   Layout L = layout(cam, ty0, ty1, p->tile_rank, p->tile_world);
   const long long n_pix = (long long)L.n_tiles_rank * kTilePixels;
 
-  // samples per unit: enough units to keep every resident lane busy ~16x over (tail < ~3%)
+  int engine = p->engine & 0xf;
+  const bool timing = (p->engine & RT_ENGINE_TIMING) != 0;
+  if (engine == RT_ENGINE_AUTO) engine = default_engine();
+  if (engine != RT_ENGINE_MEGAKERNEL && engine != RT_ENGINE_WAVEFRONT)
+    return fail(c, RT_E_INVALID, "bad engine %d", p->engine);
+
+  // samples per unit: enough units to keep every resident lane busy ~16x over (tail < ~3%);
+  // the wavefront engine keeps units short (its slots regenerate every iteration anyway)
   int chunk = p->sample_chunk;
+  if (chunk == 0 && engine == RT_ENGINE_WAVEFRONT) chunk = kWfDefaultChunk;
   if (chunk == 0) {
-    long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * kBlockThreads;
+    long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * kTraceThreads;
     long long want_units = 16 * lanes;
     long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
     n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
@@ -326,11 +521,20 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   kp.counters = static_cast<DCounters*>(c->counters.p);
 
   HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
-  HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, sizeof(DCounters), s));
-  const int blocks = std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
-  HIP_TRY(c, hipEventRecord(c->ev[0], s));
-  if (n_pix > 0) HIP_TRY(c, launch_trace(kp, blocks, s));
-  HIP_TRY(c, hipEventRecord(c->ev[1], s));
+  HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
+  c->last_engine = engine;
+  c->last_iters = 0;
+  c->last_slots = 0;
+  c->last_timing = 0;
+  if (engine == RT_ENGINE_WAVEFRONT) {
+    st = run_wavefront(c, kp, timing, s);
+    if (st) return st;
+  } else {
+    const int blocks = std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
+    HIP_TRY(c, hipEventRecord(c->ev[0], s));
+    if (n_pix > 0) HIP_TRY(c, launch_trace(kp, blocks, s));
+    HIP_TRY(c, hipEventRecord(c->ev[1], s));
+  }
   if (n_pix > 0)
     HIP_TRY(c, launch_reduce(kp.partial, n_chunks, L.n_tiles_rank, L.tiles_x, ty0, p->tile_rank, p->tile_world,
                              cam->image_width, row0, row1, packed, out_dev, s));
@@ -343,7 +547,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
 
 extern "C" {
 
-const char* rt_version(void) { return "shirley-rt 0.1 (gfx950, f64 persistent megakernel)"; }
+const char* rt_version(void) { return "shirley-rt 0.2 (gfx950, f64 wavefront + persistent megakernel)"; }
 
 int rt_device_count(int32_t* out) {
   if (!out) return RT_E_INVALID;
@@ -374,7 +578,10 @@ int rt_create(int32_t device, rt_ctx** out) {
   c->cu_count = prop.multiProcessorCount;
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return bail(RT_E_HIP);
-  if (ensure(c, c->counters, sizeof(DCounters)) || ensure(c, c->unit_counter, 64)) return bail(RT_E_OOM);
+  for (auto& e : c->wf_ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(RT_E_HIP);
+  if (hipHostMalloc((void**)&c->wf_host, 64, hipHostMallocDefault) != hipSuccess) return bail(RT_E_OOM);
+  if (ensure(c, c->counters, kCounterSlots * sizeof(DCounters)) || ensure(c, c->unit_counter, 64)) return bail(RT_E_OOM);
   *out = c;
   return RT_OK;
 }
@@ -384,10 +591,14 @@ int rt_destroy(rt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->nodes, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->partial,
-                    &c->accum, &c->counters, &c->unit_counter})
+                    &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters})
     release(*b);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->wf_ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : c->lap_ev) (void)hipEventDestroy(e);
+  if (c->wf_host) (void)hipHostFree(c->wf_host);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return RT_OK;
@@ -397,6 +608,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   if (!c) return RT_E_INVALID;
   int st = validate(c, d);
   if (st) return st;
+  const int32_t placement_mask = RT_BVH_NODES_GLOBAL | RT_BVH_NODES_HALF_LDS | RT_BVH_NODES_LDS;
+  const int32_t placement = builder & placement_mask;
+  builder &= ~placement_mask;
   if (builder != RT_BVH_REFERENCE && builder != RT_BVH_SAH) return fail(c, RT_E_INVALID, "bad bvh builder %d", builder);
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -480,11 +694,36 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.stack_depth = depth + 2;  // ordered traversal holds at most one deferred child per branch level
   S.sky = d->sky;
   for (int k = 0; k < 3; ++k) S.sky_color[k] = d->sky_color[k];
+  // LDS of one block: the traversal stacks, then (placement flags) a copy of the BVH's top levels
+  long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
+  if (stack_bytes > kLdsBytes)
+    return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
+  auto lds_nodes_for = [&](long long stack) -> int32_t {
+    long long room = std::min<long long>((kLdsBytes - stack) / (long long)sizeof(DNode), (long long)nodes.size());
+    if (placement & RT_BVH_NODES_LDS) return (int32_t)room;
+    if (placement & RT_BVH_NODES_HALF_LDS) return (int32_t)std::min<long long>(room, (long long)nodes.size() / 2);
+    return 0;  // default: nodes read through L1/L2
+  };
+  S.n_lds_nodes = lds_nodes_for(stack_bytes);
 
   int bpc = 0;
-  HIP_TRY(c, trace_occupancy(S.stack_depth, &bpc));
-  if (bpc < 1) return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
+  HIP_TRY(c, trace_occupancy(S, &bpc));
+  if (bpc < 1) return fail(c, RT_E_UNSUPPORTED, "trace kernel does not fit on a CU (LDS %lld B)", stack_bytes);
   c->blocks_per_cu = bpc;
+
+  // wavefront extend block: its own (larger) stack area, the rest of LDS for nodes
+  DScene W = S;
+  long long wf_stack = (long long)S.stack_depth * wf_extend_threads() * 8;
+  if (wf_stack > kLdsBytes)
+    return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
+  W.n_lds_nodes = lds_nodes_for(wf_stack);
+  int wbpc = 0;
+  HIP_TRY(c, wf_prepare(W, &wbpc));
+  if (wbpc < 1) return fail(c, RT_E_UNSUPPORTED, "wavefront extend kernel does not fit on a CU");
+  c->wf_scene = W;
+  c->has_perlin = false;
+  for (int i = 0; i < d->n_textures; ++i) c->has_perlin |= d->textures[i].kind == RT_TEX_PERLIN;
+  c->wf_blocks_per_cu = wbpc;
 
   c->stats.n_objects = d->n_objects;
   c->stats.n_nodes = (int32_t)tree.nodes.size();
@@ -605,17 +844,27 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
   if (!c->have_timing) return fail(c, RT_E_INVALID, "no render has run on this context");
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipEventSynchronize(c->ev[2]));
-  DCounters dc;
-  HIP_TRY(c, hipMemcpy(&dc, c->counters.p, sizeof dc, hipMemcpyDeviceToHost));
-  out->samples = dc.samples;
-  out->segments = dc.segments;
-  out->node_visits = dc.node_visits;
-  out->prim_tests = dc.prim_tests;
+  std::vector<DCounters> dc(kCounterSlots);
+  HIP_TRY(c, hipMemcpy(dc.data(), c->counters.p, kCounterSlots * sizeof(DCounters), hipMemcpyDeviceToHost));
+  for (const DCounters& k : dc) {
+    out->samples += k.samples;
+    out->segments += k.segments;
+    out->node_visits += k.node_visits;
+    out->prim_tests += k.prim_tests;
+  }
   float a = 0.f, b = 0.f;
   HIP_TRY(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
   HIP_TRY(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
   out->kernel_ms = a;
   out->reduce_ms = b;
+  out->engine = c->last_engine;
+  out->iterations = c->last_iters;
+  out->slots = c->last_slots;
+  if (c->last_timing) {
+    out->extend_ms = c->lap_ms[0];
+    out->shade_ms = c->lap_ms[1];
+    out->texture_ms = c->lap_ms[2];
+  }
   return RT_OK;
 }
 

@@ -1,0 +1,608 @@
+// rt_device.h — device functions of the hot path shared by the megakernel (trace.hip) and the
+// wavefront kernels (wavefront.hip): f64 vector algebra in nalgebra's order, the counter RNG,
+// intersection, BVH traversal, textures, materials, camera.  Semantics follow the reference line by
+// line (citations inline); compiled with -ffp-contract=off (Rust never fuses a*b+c).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "../../../include/shirley_rt.h"
+#include "rt_layout.h"
+
+namespace rt {
+
+
+// ------------------------------------------------------------------------------------------
+// f64 vector algebra in nalgebra's evaluation order (core/vec3.rs over nalgebra 0.31)
+// ------------------------------------------------------------------------------------------
+struct v3 {
+  double x, y, z;
+};
+__device__ __forceinline__ v3 V(double x, double y, double z) { return v3{x, y, z}; }
+__device__ __forceinline__ v3 operator+(v3 a, v3 b) { return V(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ v3 operator-(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ v3 hmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ v3 scale(v3 a, double s) { return V(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ double dot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ double len2(v3 a) { return dot(a, a); }
+__device__ __forceinline__ double len(v3 a) { return sqrt(len2(a)); }
+__device__ __forceinline__ v3 unit(v3 a) {
+  double n = len(a);
+  return V(a.x / n, a.y / n, a.z / n);
+}
+__device__ __forceinline__ double comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+// vec3.rs:129-132
+__device__ __forceinline__ bool near_zero(v3 a) {
+  return fabs(a.x) < 1e-8 && fabs(a.y) < 1e-8 && fabs(a.z) < 1e-8;
+}
+// vec3.rs:134-137
+__device__ __forceinline__ v3 reflect(v3 v, v3 n) { return v - scale(n, 2.0 * dot(v, n)); }
+// fp.rs:3-11 fmin (NaN-aware) specialised to fmin(x, 1.0) = math.rs:16-19 fmin_one
+__device__ __forceinline__ double fmin_one(double x) { return (x < 1.0) ? x : 1.0; }
+// vec3.rs:139-145
+__device__ __forceinline__ v3 refract(v3 uv, v3 n, double eta) {
+  double cos_theta = fmin_one(dot(scale(uv, -1.0), n));
+  v3 r_out_perp = scale(scale(n, cos_theta) + uv, eta);
+  double r_out_parallel_mag = sqrt(fabs(1.0 - len2(r_out_perp))) * -1.0;
+  return r_out_perp + scale(n, r_out_parallel_mag);
+}
+
+// ------------------------------------------------------------------------------------------
+// counter-based RNG: Philox4x32-10 keyed by seed, counter (draw/2, sample, pixel, 0).
+// A draw is converted like rand 0.8's Standard f64: (u64 >> 11) * 2^-53.
+// ------------------------------------------------------------------------------------------
+struct Rng {
+  uint32_t pixel, sample, draw, c2, c3;
+};
+__device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
+                                         uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+}
+__device__ __forceinline__ double rng_next(Rng& r, uint64_t seed) {
+  uint64_t v;
+  if ((r.draw & 1u) == 0u) {
+    uint32_t c0 = r.draw >> 1, c1 = r.sample, c2 = r.pixel, c3 = 0u;
+    philox10(c0, c1, c2, c3, (uint32_t)seed, (uint32_t)(seed >> 32));
+    v = (uint64_t)c0 | ((uint64_t)c1 << 32);
+    r.c2 = c2;
+    r.c3 = c3;
+  } else {
+    v = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
+  }
+  r.draw++;
+  return (double)(v >> 11) * (1.0 / 9007199254740992.0);
+}
+// core/math.rs:22-25
+__device__ __forceinline__ double random_real(Rng& r, uint64_t seed, double mn, double mx) {
+  return mn + (mx - mn) * rng_next(r, seed);
+}
+// core/math.rs:32-45 (+ vec3.rs:104-110)
+__device__ __forceinline__ v3 random_in_unit_sphere(Rng& r, uint64_t seed) {
+  for (;;) {
+    double x = random_real(r, seed, -1.0, 1.0);
+    double y = random_real(r, seed, -1.0, 1.0);
+    double z = random_real(r, seed, -1.0, 1.0);
+    v3 p = V(x, y, z);
+    if (len2(p) <= 1.0) return p;
+  }
+}
+// core/math.rs:70-81
+__device__ __forceinline__ v3 random_in_unit_disk(Rng& r, uint64_t seed) {
+  for (;;) {
+    double x = random_real(r, seed, -1.0, 1.0);
+    double y = random_real(r, seed, -1.0, 1.0);
+    v3 p = V(x, y, 0.0);
+    if (len2(p) <= 1.0) return p;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// intersection (t only during traversal; the full hit record is rebuilt for the winner)
+// ------------------------------------------------------------------------------------------
+// aabb.rs:62-79 hit2; axes evaluated without early exit (t_min only grows, t_max only shrinks,
+// so the final `t_max <= t_min` test equals the reference's per-axis early return).
+__device__ __forceinline__ bool slab(const double* b, v3 o, v3 inv, double t_min, double t_max, double& t_enter) {
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    double iv = comp(inv, a);
+    double t0 = (b[a] - comp(o, a)) * iv;
+    double t1 = (b[a + 3] - comp(o, a)) * iv;
+    if (iv < 0.0) {
+      double tmp = t0;
+      t0 = t1;
+      t1 = tmp;
+    }
+    t_min = (t0 > t_min) ? t0 : t_min;
+    t_max = (t1 < t_max) ? t1 : t_max;
+  }
+  t_enter = t_min;
+  return !(t_max <= t_min);
+}
+
+// sphere.rs:28-46 (t only)
+__device__ __forceinline__ bool sphere_t(const double* p, v3 o, v3 d, double a, double t_min, double t_max,
+                                         double& t) {
+  v3 oc = o - V(p[0], p[1], p[2]);
+  double half_b = dot(oc, d);
+  double c = len2(oc) - p[3] * p[3];
+  double disc = half_b * half_b - a * c;
+  if (disc < 0.0) return false;
+  double sqrt_d = sqrt(disc);
+  double root = (-half_b - sqrt_d) / a;
+  if (root < t_min || t_max < root) {
+    root = (-half_b + sqrt_d) / a;
+    if (root < t_min || t_max < root) return false;
+  }
+  t = root;
+  return true;
+}
+
+// rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset
+template <int D1, int D2>
+__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out) {
+  constexpr int n = 3 - D1 - D2;
+  double t = (q[4] - comp(o, n)) / comp(d, n);
+  if (t < t_min || t > t_max) return false;
+  double d1v = comp(o, D1) + t * comp(d, D1);
+  double d2v = comp(o, D2) + t * comp(d, D2);
+  if (d1v < q[0] || d1v > q[1] || d2v < q[2] || d2v > q[3]) return false;
+  t_out = t;
+  return true;
+}
+
+// rect.rs:132-156 RectBox::hit — six faces in order, each against the running closest.
+// Returns the face index (0..5) that won, or -1.
+__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out) {
+  double q[5];
+  int face = -1;
+  double tc = t_max, t;
+  // xy_sides: (p0.x, p1.x, p0.y, p1.y, p1.z), (..., p0.z)
+  q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
+  q[4] = b[5];
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 0; }
+  q[4] = b[2];
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 1; }
+  // yz_sides: (p0.y, p1.y, p0.z, p1.z, p1.x), (..., p0.x)
+  q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
+  q[4] = b[3];
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 2; }
+  q[4] = b[0];
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 3; }
+  // xz_sides: (p0.x, p1.x, p0.z, p1.z, p1.y), (..., p0.y)
+  q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
+  q[4] = b[4];
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 4; }
+  q[4] = b[1];
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 5; }
+  t_out = tc;
+  return face;
+}
+
+__device__ __forceinline__ bool prim_t(const DPrim& pr, v3 o, v3 d, double a, double t_min, double t_max, double& t,
+                                       int& face) {
+  switch (pr.kind) {
+    case kPrimSphere: return sphere_t(pr.p, o, d, a, t_min, t_max, t);
+    case kPrimRectXY: return rect_t<0, 1>(pr.p, o, d, t_min, t_max, t);
+    case kPrimRectYZ: return rect_t<1, 2>(pr.p, o, d, t_min, t_max, t);
+    case kPrimRectXZ: return rect_t<0, 2>(pr.p, o, d, t_min, t_max, t);
+    default: {
+      face = box_t(pr.p, o, d, t_min, t_max, t);
+      return face >= 0;
+    }
+  }
+}
+
+struct Hit {
+  v3 point, normal;
+  double t, u, v;
+  bool front_face;
+};
+
+// hittable.rs:16-38
+__device__ __forceinline__ void finish_hit(Hit& h, v3 d, v3 normal) {
+  h.front_face = dot(d, normal) < 0.0;
+  h.normal = h.front_face ? normal : scale(normal, -1.0);
+}
+
+// sphere.rs:17-26 get_uv — acos/atan2 kept out of line to hold the kernel's register budget.
+struct UV {
+  double u, v;
+};
+__device__ __noinline__ UV sphere_uv(double nx, double ny, double nz) {
+  double theta = acos(-ny);
+  double phi = atan2(-nz, nx) + 3.14159265358979323846;
+  return UV{phi / (2.0 * 3.14159265358979323846), theta / 3.14159265358979323846};
+}
+
+// Rebuild the winner's HitRecord with the exact reference formulas (same t => same record).
+// Written with scalars only (no local arrays) so that nothing is demoted to scratch memory.
+// WANT_UV = false skips u, v (only image textures read them; sphere u, v cost an acos + atan2).
+template <bool WANT_UV = true>
+__device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 d, double t, Hit& h) {
+  h.t = t;
+  h.point = o + scale(d, t);  // ray.at(t) (vec3.rs:253-255)
+  v3 normal;
+  double u = 0.0, v = 0.0;
+  if (pr.kind == kPrimSphere) {
+    // sphere.rs:46-51 + get_uv 17-26: u, v from the outward normal (p - c) / r (signed r)
+    normal = scale(h.point - V(pr.p[0], pr.p[1], pr.p[2]), 1.0 / pr.p[3]);
+    if (WANT_UV) {
+      UV uv = sphere_uv(normal.x, normal.y, normal.z);
+      u = uv.u;
+      v = uv.v;
+    }
+  } else {
+    // rect.rs:66-79; a RectBox face is the rect of RectBox::new with the face's offset
+    const double* b = pr.p;
+    int kind = pr.kind;
+    double q0 = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
+    if (kind == kPrimBox) {
+      if (face < 2) { q0 = b[0]; q1 = b[3]; q2 = b[1]; q3 = b[4]; kind = kPrimRectXY; }
+      else if (face < 4) { q0 = b[1]; q1 = b[4]; q2 = b[2]; q3 = b[5]; kind = kPrimRectYZ; }
+      else { q0 = b[0]; q1 = b[3]; q2 = b[2]; q3 = b[5]; kind = kPrimRectXZ; }
+    }
+    double o1, d1, o2, d2;
+    if (kind == kPrimRectXY) { o1 = o.x; d1 = d.x; o2 = o.y; d2 = d.y; normal = V(0.0, 0.0, 1.0); }
+    else if (kind == kPrimRectYZ) { o1 = o.y; d1 = d.y; o2 = o.z; d2 = d.z; normal = V(1.0, 0.0, 0.0); }
+    else { o1 = o.x; d1 = d.x; o2 = o.z; d2 = d.z; normal = V(0.0, 1.0, 0.0); }
+    if (WANT_UV) {
+      double d1v = o1 + t * d1;
+      double d2v = o2 + t * d2;
+      u = (d1v - q0) / (q1 - q0);
+      v = (d2v - q2) / (q3 - q2);
+    }
+  }
+  h.u = u;
+  h.v = v;
+  finish_hit(h, d, normal);
+}
+
+// ------------------------------------------------------------------------------------------
+// BVH traversal: closest hit in [t_min, t_max] (bbox_tree.rs:56-91 semantics, near-first order)
+// ------------------------------------------------------------------------------------------
+// Traversal state of one ray.
+struct Trav {
+  v3 inv;         // 1/d per axis (aabb.rs:66 computes the same quotient per call)
+  double a;       // |d|^2 (sphere.rs:31)
+  double t_best;  // closest accepted t so far (t_max initially)
+  int best, face, node, sp;
+};
+
+__device__ __forceinline__ void trav_begin(Trav& T, v3 d, double t_max) {
+  T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  T.a = len2(d);
+  T.t_best = t_max;
+  T.best = -1;
+  T.face = -1;
+  T.node = 0;  // top node: child[0] = root
+  T.sp = 0;
+}
+
+// Node source by kernel instance: all nodes in LDS, all in HBM/L2, or the first n_lds_nodes (BFS
+// order: the top levels) in LDS and the rest in HBM.  Separate instances keep LDS reads ds_read
+// (a select between an LDS and a global pointer would make every read a FLAT load).
+template <int MODE>
+__device__ __forceinline__ const DNode& fetch_node(const DScene& S, const DNode* lds_nodes, int idx) {
+  if (MODE == kNodesLds) return lds_nodes[idx];
+  if (MODE == kNodesGlobal) return S.nodes[idx];
+  return (idx < S.n_lds_nodes) ? lds_nodes[idx] : S.nodes[idx];
+}
+
+// A leaf child whose (exact) box was hit: the object against the running closest (bbox_tree.rs:60-71).
+__device__ __forceinline__ void leaf_visit(const DScene& S, int prim, v3 o, v3 d, double t_min, Trav& T,
+                                           unsigned& ptests) {
+  const DPrim& pr = S.prims[prim];
+  double t;
+  int f = -1;
+  ++ptests;
+  if (prim_t(pr, o, d, T.a, t_min, T.t_best, t, f)) {
+    T.t_best = t;
+    T.best = prim;
+    T.face = f;
+  }
+}
+
+// Visit node T.node: test both child boxes (f64 hit2 on the reference's boxes), visit hit leaf
+// children at once (they can shrink t_best for the sibling), descend into the nearer hit internal
+// child and push the farther.  Returns true when the traversal is complete (T.best / T.t_best /
+// T.face hold the closest hit).  Stack: per-lane, in LDS, [depth][lane] with a stride of the block
+// size (bank = lane % 32); entry t rounded down to f32 (only ever compared against t_best).
+template <int STRIDE, int MODE>
+__device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_nodes, v3 o, v3 d, double t_min, Trav& T,
+                                          int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
+  const DNode& nd = fetch_node<MODE>(S, lds_nodes, T.node);
+  const int c0 = nd.child[0], c1 = nd.child[1];
+  double te0 = 0.0, te1 = 0.0;
+  bool h0 = (c0 != kEmptyChild) && slab(nd.box[0], o, T.inv, t_min, T.t_best, te0);
+  bool h1 = (c1 != kEmptyChild) && slab(nd.box[1], o, T.inv, t_min, T.t_best, te1);
+  visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
+  // leaf children (one primitive each)
+  if (h0 && c0 < 0) {
+    leaf_visit(S, ~c0, o, d, t_min, T, ptests);
+    h0 = false;
+  }
+  if (h1 && c1 < 0) {
+    leaf_visit(S, ~c1, o, d, t_min, T, ptests);
+    h1 = false;
+  }
+  int next;
+  if (h0 && h1) {
+    const bool first0 = te0 <= te1;
+    next = first0 ? c0 : c1;
+    stk_node[T.sp * STRIDE] = first0 ? c1 : c0;
+    stk_t[T.sp * STRIDE] = __double2float_rd(first0 ? te1 : te0);
+    ++T.sp;
+  } else if (h0 || h1) {
+    next = h0 ? c0 : c1;
+  } else {
+    next = -1;
+    while (T.sp > 0) {
+      --T.sp;
+      // a pushed subtree whose entry lies beyond the current closest hit cannot hold it
+      if ((double)stk_t[T.sp * STRIDE] <= T.t_best) {
+        next = stk_node[T.sp * STRIDE];
+        break;
+      }
+    }
+    if (next < 0) return true;
+  }
+  T.node = next;
+  return false;
+}
+
+// Whole closest-hit query (WorkspaceScene::hit_workspace, scene/mod.rs:152-164; the unbounded
+// HitList is always empty because every geometry is bounded).  Same visit order and tests as
+// trav_step, written as one loop over locals: the megakernel holds a whole path's state beside the
+// traversal, and this form keeps the traversal's registers out of scratch.
+template <int STRIDE, int MODE>
+__device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes, v3 o, v3 d, double t_min,
+                                        double& t_best, int& face_best, int* stk_node, float* stk_t,
+                                        unsigned& visits, unsigned& ptests) {
+  const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  const double a = len2(d);
+  int best = -1;
+  int sp = 0;
+  int node = 0;  // top node: child[0] = root
+  for (;;) {
+    const DNode& nd = fetch_node<MODE>(S, lds_nodes, node);
+    const int c0 = nd.child[0], c1 = nd.child[1];
+    double te0 = 0.0, te1 = 0.0;
+    bool h0 = (c0 != kEmptyChild) && slab(nd.box[0], o, inv, t_min, t_best, te0);
+    bool h1 = (c1 != kEmptyChild) && slab(nd.box[1], o, inv, t_min, t_best, te1);
+    visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
+    if (h0 && c0 < 0) {
+      const DPrim& pr = S.prims[~c0];
+      double t;
+      int f = -1;
+      ++ptests;
+      if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = ~c0; face_best = f; }
+      h0 = false;
+    }
+    if (h1 && c1 < 0) {
+      const DPrim& pr = S.prims[~c1];
+      double t;
+      int f = -1;
+      ++ptests;
+      if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = ~c1; face_best = f; }
+      h1 = false;
+    }
+    int next;
+    if (h0 && h1) {
+      const bool first0 = te0 <= te1;
+      next = first0 ? c0 : c1;
+      stk_node[sp * STRIDE] = first0 ? c1 : c0;
+      stk_t[sp * STRIDE] = __double2float_rd(first0 ? te1 : te0);
+      ++sp;
+    } else if (h0) {
+      next = c0;
+    } else if (h1) {
+      next = c1;
+    } else {
+      next = -1;
+      while (sp > 0) {
+        --sp;
+        if ((double)stk_t[sp * STRIDE] <= t_best) {
+          next = stk_node[sp * STRIDE];
+          break;
+        }
+      }
+      if (next < 0) break;
+    }
+    node = next;
+  }
+  return best;
+}
+
+// Copy nodes [0, n_lds_nodes) into the block's LDS node cache (16-B coalesced loads).
+template <int MODE>
+__device__ __forceinline__ void stage_nodes(const DScene& S, DNode* lds_nodes) {
+  if (MODE == kNodesGlobal) return;
+  const int4* src = reinterpret_cast<const int4*>(S.nodes);
+  int4* dst = reinterpret_cast<int4*>(lds_nodes);
+  const int n16 = S.n_lds_nodes * (int)(sizeof(DNode) / 16);
+  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------------
+// textures (material/texture/*.rs, perlin/mod.rs) and materials
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t sat_i32(double x) {
+  if (x != x) return 0;
+  if (x >= 2147483647.0) return 2147483647;
+  if (x <= -2147483648.0) return (int32_t)(-2147483647 - 1);
+  return (int32_t)x;
+}
+
+// perlin/mod.rs:87-109 + interp 40-63
+__device__ __noinline__ double perlin_noise(const DPerlin* T, v3 p) {
+  double xf = floor(p.x), yf = floor(p.y), zf = floor(p.z);
+  double u = p.x - xf, v = p.y - yf, w = p.z - zf;
+  uint32_t i = (uint32_t)sat_i32(xf), j = (uint32_t)sat_i32(yf), k = (uint32_t)sat_i32(zf);
+  double uu = u * u * (3.0 - 2.0 * u);
+  double vv = v * v * (3.0 - 2.0 * v);
+  double ww = w * w * (3.0 - 2.0 * w);
+  double accum = 0.0;
+#pragma unroll 1
+  for (int di = 0; di < 2; ++di) {
+    double fi = (double)di;
+    int px = T->perm_x[(i + di) & 0xFF];
+#pragma unroll 1
+    for (int dj = 0; dj < 2; ++dj) {
+      double fj = (double)dj;
+      int pxy = px ^ T->perm_y[(j + dj) & 0xFF];
+#pragma unroll 1
+      for (int dk = 0; dk < 2; ++dk) {
+        double fk = (double)dk;
+        int idx = pxy ^ T->perm_z[(k + dk) & 0xFF];
+        v3 c = V(T->ranfloat[idx][0], T->ranfloat[idx][1], T->ranfloat[idx][2]);
+        v3 weight = V(u - fi, v - fj, w - fk);
+        accum += (fi * uu + (1.0 - fi) * (1.0 - uu)) * (fj * vv + (1.0 - fj) * (1.0 - vv)) *
+                 (fk * ww + (1.0 - fk) * (1.0 - ww)) * dot(c, weight);
+      }
+    }
+  }
+  return accum;
+}
+
+// perlin/mod.rs:162-183 NoiseTexture::value ("marble"): 0.5 (1 + sin(scale p.z + 10 turb(p, 7)));
+// the x/y terms of the reference's dot with (0,0,1) contribute exactly 0.
+__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) {
+  double accum = 0.0;
+  v3 tp = p;
+  double weight = 1.0;
+  for (int i = 0; i < 7; ++i) {  // turbulence, perlin/mod.rs:111-124
+    accum += weight * perlin_noise(T, tp);
+    weight *= 0.5;
+    tp = scale(tp, 2.0);
+  }
+  double turb = 10.0 * fabs(accum);
+  double total_noise = sin(sc * p.z + turb);
+  return 0.5 * (1.0 + total_noise);
+}
+
+// checker.rs:28-30
+__device__ __noinline__ double checker_sines(double s, double x, double y, double z) {
+  return sin(s * x) * sin(s * y) * sin(s * z);
+}
+
+__device__ __forceinline__ v3 texture_value(const DScene& S, int ti, double u, double v, v3 p) {
+  for (;;) {
+    const DTex& t = S.texs[ti];
+    if (t.kind == RT_TEX_SOLID) return V(t.color[0], t.color[1], t.color[2]);  // solid.rs:17-21
+    if (t.kind == RT_TEX_CHECKER) {                                             // checker.rs:27-37
+      double sines = checker_sines(t.scale, p.x, p.y, p.z);
+      ti = (sines < 0.0) ? t.odd : t.even;
+      continue;
+    }
+    if (t.kind == RT_TEX_PERLIN) {
+      double n = marble(S.perlin + t.table, t.scale, p);
+      return V(n, n, n);
+    }
+    // image_texture.rs:34-56: clamp, flip v, truncate, /255
+    const DImage im = S.images[t.table];
+    double uu = (u > 0.0) ? ((u < 1.0) ? u : 1.0) : 0.0;
+    double vv = 1.0 - ((v > 0.0) ? ((v < 1.0) ? v : 1.0) : 0.0);
+    uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
+    uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
+    const uint8_t* px = S.texels + im.offset + ((size_t)iy * (size_t)im.width + ix) * 3;
+    const double cs = 1.0 / 255.0;
+    return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
+  }
+}
+
+// dielectric.rs:15-19
+__device__ __noinline__ double reflectance(double cosine, double ref_idx) {
+  double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
+  r0 = r0 * r0;
+  return r0 + (1.0 - r0) * pow(1.0 - cosine, 5.0);
+}
+
+// skybox/mod.rs:5-25
+__device__ __forceinline__ v3 sky(const DScene& S, v3 d) {
+  if (S.sky == RT_SKY_ABOVE) {
+    v3 un = unit(d);
+    double t = 0.5 * (un.y + 1.0);
+    return scale(V(1.0, 1.0, 1.0), 1.0 - t) + scale(V(0.5, 0.7, 1.0), t);
+  }
+  if (S.sky == RT_SKY_FLAT) return V(S.sky_color[0], S.sky_color[1], S.sky_color[2]);
+  return V(0.0, 0.0, 0.0);
+}
+
+// One ray_color loop iteration after the hit (render.rs:31-40): emitted, then scatter.
+// Returns false when the path ends (material absorbed).  Metal, Lambertian and FairyLight all draw
+// random_in_unit_sphere (metal.rs:32, lambertian.rs:23 via random_unit_vector); it has one call site.
+__device__ __forceinline__ bool shade(const DScene& S, const DMat& m, Rng& rng, uint64_t seed, v3& o, v3& d,
+                                      const Hit& h, v3& att, v3& em) {
+  if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
+    v3 e = texture_value(S, m.tex, h.u, h.v, h.point);
+    em = em + hmul(att, e);
+    return false;
+  }
+  if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
+    double ratio = h.front_face ? (1.0 / m.param) : m.param;
+    v3 ud = unit(d);
+    double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
+    double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+    bool refl = ratio * sin_theta > 1.0;
+    if (!refl) refl = reflectance(cos_theta, ratio) > rng_next(rng, seed);  // drawn only if not TIR
+    o = h.point;
+    d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
+    return true;  // attenuation = Color::ones()
+  }
+  v3 r = random_in_unit_sphere(rng, seed);
+  if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
+    v3 reflected = reflect(unit(d), h.normal);
+    o = h.point;
+    d = reflected + scale(r, m.param);
+    att = hmul(att, V(m.albedo[0], m.albedo[1], m.albedo[2]));
+    return true;
+  }
+  // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
+  v3 a = texture_value(S, m.tex, h.u, h.v, h.point);
+  if (m.kind == RT_MAT_FAIRY_LIGHT) {
+    double s = dot(h.normal, scale(d, -1.0));
+    em = em + hmul(att, scale(a, s / len(d)));
+    a = unit(a);
+  }
+  v3 sc = h.normal + unit(r);
+  if (near_zero(sc)) sc = h.normal;
+  o = h.point;
+  d = sc;
+  att = hmul(att, a);
+  return true;
+}
+
+// camera/mod.rs:97-132 (horizontal / vertical / lower_left precomputed on the host, same ops)
+__device__ __forceinline__ void camera_ray(const DCamera& C, Rng& rng, uint64_t seed, double x, double y, v3& o,
+                                           v3& d) {
+  double xp = x / (double)C.width;
+  double yp = y / (double)C.height;
+  v3 u = V(C.u[0], C.u[1], C.u[2]), v = V(C.v[0], C.v[1], C.v[2]);
+  v3 origin = V(C.origin[0], C.origin[1], C.origin[2]);
+  v3 offset = V(0.0, 0.0, 0.0);
+  if (C.has_lens) {
+    v3 rd = scale(random_in_unit_disk(rng, seed), C.lens_radius);
+    offset = scale(u, rd.x) + scale(v, rd.y);
+  }
+  v3 ll = V(C.lower_left[0], C.lower_left[1], C.lower_left[2]);
+  v3 hz = V(C.horizontal[0], C.horizontal[1], C.horizontal[2]);
+  v3 vt = V(C.vertical[0], C.vertical[1], C.vertical[2]);
+  d = (((ll + scale(hz, xp)) + scale(vt, yp)) - origin) - offset;
+  o = origin + offset;
+}
+
+
+}  // namespace rt

@@ -12,19 +12,26 @@ namespace rt {
 // Tile geometry: a wave (64 lanes) owns an 8x8 pixel tile of one sample chunk.
 constexpr int kTile = 8;
 constexpr int kTilePixels = kTile * kTile;  // == wavefront size
-constexpr int kBlockThreads = 256;          // 4 waves per workgroup
+constexpr int kTraceThreads = 256;  // megakernel block: 4 waves (several blocks per CU)
+constexpr int kHitThreads = 256;    // rt_scene_hit kernel
 constexpr int kWave = 64;
+constexpr int kLdsBytes = 160 * 1024;  // LDS per CU (gfx950)
 
-// BVH2 node with both child boxes inline (one 112-B record per internal node).
+// BVH2 node with both child boxes inline (one 112-B record per internal node).  The boxes are the
+// reference's exact f64 bounding boxes, so testing a child box with the f64 slab test IS the
+// reference's Aabb::hit2 on that child (bbox_tree.rs:60-71): for a leaf child that is the test of
+// the object's own bounding_box() before the object itself.
 // child >= 0: internal node index; child < 0: leaf, primitive index = ~child; kEmptyChild: none.
 constexpr int32_t kEmptyChild = 0x7fffffff;
 struct alignas(16) DNode {
-  // child c: lo = {box[c][0..2]}, hi = {box[c][3..5]}
-  double box[2][6];
+  double box[2][6];  // child c: lo = box[c][0..2], hi = box[c][3..5]
   int32_t child[2];
   int32_t pad[2];
 };
 static_assert(sizeof(DNode) == 112, "DNode layout");
+
+// Where a kernel instance reads BVH nodes from (template parameter of the traversal):
+enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2 };
 
 // Primitive kinds (device-side, rect axis folded into the kind).
 enum : int32_t { kPrimSphere = 0, kPrimRectXY = 1, kPrimRectYZ = 2, kPrimRectXZ = 3, kPrimBox = 4 };
@@ -74,6 +81,7 @@ struct DScene {
   const uint8_t* texels;
   int32_t n_nodes, n_prims;
   int32_t stack_depth;     // max stack entries a traversal can need
+  int32_t n_lds_nodes;     // nodes [0, n_lds_nodes) are copied into LDS per block (BFS order: top levels)
   int32_t sky;
   double sky_color[3];
 };
@@ -101,9 +109,13 @@ struct DWork {
   uint64_t n_units;              // n_tiles_rank * n_chunks * 64
 };
 
+// Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot
+// blockIdx % kCounterSlots, so atomics from different blocks do not serialise on one address.
 struct DCounters {
   unsigned long long samples, segments, node_visits, prim_tests;
+  unsigned long long pad[12];
 };
+constexpr int kCounterSlots = 64;
 
 struct KParams {
   DScene scene;
@@ -112,6 +124,54 @@ struct KParams {
   double* partial;               // [n_chunks][n_tiles_rank*64][3]
   unsigned long long* unit_counter;  // work-queue head (one 64-unit batch per fetch)
   DCounters* counters;
+};
+
+// ---- wavefront engine (wavefront.hip): path state of P slots as structure-of-arrays in HBM ----
+struct WfState {
+  double *ox, *oy, *oz, *dx, *dy, *dz;  // ray to trace
+  double *ax, *ay, *az;                 // throughput of the current sample
+  double *ex, *ey, *ez;                 // radiance of the current sample
+  double *sx, *sy, *sz;                 // in-order sum of the unit's finished samples
+  double* ht;                           // closest hit t
+  uint64_t* part;                       // partial-sum slot of the unit
+  uint32_t* pixel;                      // rng pixel id (py * W + px), 0xffffffff: no unit
+  uint32_t *sample, *draw, *c2, *c3;    // rng counter state of the current sample
+  int32_t *s_next, *s_end;              // next sample to start / end of the unit
+  int32_t* depth;                       // bounces left
+  int32_t *hprim, *hface;               // closest primitive (-1: miss), RectBox face
+  uint8_t* state;
+};
+constexpr size_t kWfSlotBytes = 16 * 8 + 8 + 11 * 4 + 1;  // bytes of one slot across the arrays
+
+struct WfTexQ {  // deferred (Perlin) texture evaluations, compacted per 64-slot group
+  double *px, *py, *pz, *scale;
+  int32_t *slot, *tex, *kind;
+  uint32_t* count;  // entries of each group this round
+};
+constexpr size_t kWfTexBytes = 4 * 8 + 3 * 4;
+
+// wf_extend hands out slots from kWfQueues cursors (one 128-B line each, zeroed every round);
+// queue q covers slots [q * qlen, (q + 1) * qlen).  A wave starts on queue (wave id % kWfQueues)
+// and moves on when it is drained, so the fetch atomics spread over kWfQueues addresses.
+constexpr int kWfQueues = 64;
+struct WfIter {
+  unsigned long long fetch[kWfQueues][16];
+};
+
+struct WfParams {
+  DScene scene;
+  DCamera cam;
+  DWork work;
+  WfState st;
+  WfTexQ tq;
+  uint32_t n_slots;     // multiple of 64: slot group g = slots [64 g, 64 g + 64) = one wave of wf_shade
+  uint32_t first;       // wf_shade's first round: group g's unit window is [64 g, 64 g + 64)
+  double* partial;
+  unsigned long long* unit_counter;  // dynamic units are n_slots + the counter (64 per fetch)
+  unsigned long long* win;           // per group: [next, end) of its unit window
+  unsigned* retired;                 // slots with no work left (== n_slots: frame done)
+  DCounters* counters;               // [kCounterSlots]
+  WfIter* it;
 };
 
 }  // namespace rt

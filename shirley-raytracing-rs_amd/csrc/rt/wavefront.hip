@@ -1,0 +1,532 @@
+// wavefront.hip — wavefront path tracer for the reference's ray_color() loop (MI355X, gfx950).
+//
+// The bounce loop of render.rs:17-48 is cut into three kernels per iteration over a pool of P path
+// slots whose state lives in HBM as structure-of-arrays (coalesced: consecutive lanes = consecutive
+// slots):
+//   wf_extend  — closest hit for every slot holding a ray (bbox_tree.rs:56-91).  Persistent waves
+//                with dynamic ray fetch: a lane whose traversal ends writes its hit and takes the
+//                next slot at once, so traversal runs with (almost) full waves; one node step per
+//                loop iteration, BVH top levels + per-lane stacks in LDS.
+//   wf_shade   — one lane per slot: emitted + scatter (material_type.rs:51-79) with the hit
+//                record rebuilt from (t, prim, face); a finished path adds its radiance to its
+//                unit's in-order sum and the slot immediately starts its next sample / takes the
+//                next unit (render.rs:58-69): path regeneration, no compaction pass needed.
+//                Texture values whose leaf is Perlin noise (perlin/mod.rs:162-183, ~7x8 gathers +
+//                sin in f64) are NOT evaluated here: they are appended to a queue...
+//   wf_texture — ...and evaluated by full, coherent waves, then folded into the slot's throughput /
+//                radiance (the next ray does not need them; the next shade does).
+// Arithmetic is binary64 and identical to the megakernel (rt_device.h), so both engines produce the
+// same pixels; counter-based RNG keyed by (pixel, sample) makes them independent of scheduling.
+#include "rt_device.h"
+
+namespace rt {
+
+enum : uint8_t { kSlotIdle = 0, kSlotAlive = 1, kSlotEnded = 2, kSlotRetired = 3 };
+enum : int32_t { kDeferLambertian = 0, kDeferFairy = 1, kDeferDiffuse = 2 };
+constexpr uint32_t kNoUnit = 0xffffffffu;
+constexpr int kExtendThreads = 256;  // 4 waves per block, several blocks per CU
+constexpr int kGridThreads = 256;
+
+__device__ __forceinline__ unsigned long long wf_lanemask_lt() {
+  unsigned lane = __lane_id();
+  return (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+}
+
+// ------------------------------------------------------------------------------------------
+// wf_extend
+// ------------------------------------------------------------------------------------------
+// Next 64-slot window for a wave: queue q first, then the following queues once q is drained.
+// Returns the window's first slot, or ~0 when every queue is drained.  Lane 0 does the work.
+__device__ __forceinline__ unsigned long long next_window(WfIter* it, int& q, uint32_t qlen) {
+  unsigned long long base = ~0ull;
+  int qq = q;
+  if (__lane_id() == 0) {
+    for (int tries = 0; tries < kWfQueues; ++tries) {
+      unsigned long long* cur = &it->fetch[qq][0];
+      if (__hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < qlen) {
+        const unsigned long long nb = atomicAdd(cur, (unsigned long long)kWave);
+        if (nb < qlen) {
+          base = (unsigned long long)qq * qlen + nb;
+          break;
+        }
+      }
+      qq = (qq + 1) % kWfQueues;
+    }
+  }
+  q = __shfl(qq, 0);
+  return __shfl(base, 0);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
+  extern __shared__ unsigned char lds_raw[];
+  const int tid = threadIdx.x;
+  DNode* lds_nodes = reinterpret_cast<DNode*>(lds_raw);
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes * sizeof(DNode);
+  int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
+  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth * kExtendThreads * 4) + tid;
+  stage_nodes<MODE>(P.scene, lds_nodes);
+  const DScene& S = P.scene;
+  const WfState& st = P.st;
+  const int lane = __lane_id();
+  const uint32_t qlen = (P.n_slots / kWfQueues + kWave) / kWave * kWave;  // multiple of 64, covers n_slots
+  int q = (int)((blockIdx.x * (kExtendThreads / kWave) + tid / kWave) % kWfQueues);
+
+  unsigned long long w_next = 0, w_end = 0;
+  bool exhausted = false, active = false;
+  int slot = 0;
+  v3 o = V(0, 0, 0), d = V(0, 0, 0);
+  Trav T;
+  unsigned visits = 0, ptests = 0, rays = 0;
+  for (;;) {
+    // lanes without a ray take the next slots of the wave's window
+    const bool need = !active;
+    const unsigned long long mask = __ballot(need);
+    if (mask != 0ull && !exhausted) {
+      if (w_next == w_end) {
+        const unsigned long long nb = next_window(P.it, q, qlen);
+        if (nb == ~0ull) {
+          exhausted = true;
+        } else {
+          w_next = nb;
+          w_end = nb + kWave;
+        }
+      }
+      if (!exhausted) {
+        const unsigned long long avail = w_end - w_next;
+        const unsigned long long rank = __popcll(mask & wf_lanemask_lt());
+        const unsigned long long idx = w_next + rank;
+        w_next += min((unsigned long long)__popcll(mask), avail);
+        if (need && rank < avail && idx < P.n_slots && st.state[idx] == kSlotAlive) {
+          slot = (int)idx;
+          o = V(st.ox[slot], st.oy[slot], st.oz[slot]);
+          d = V(st.dx[slot], st.dy[slot], st.dz[slot]);
+          trav_begin(T, d, __builtin_inf());
+          active = true;
+          ++rays;
+        }
+      }
+    }
+    if (!__any(active)) {
+      if (exhausted) break;
+      continue;
+    }
+    if (active && trav_step<kExtendThreads, MODE>(S, lds_nodes, o, d, 0.001, T, stk_node, stk_t, visits, ptests)) {
+      st.ht[slot] = T.t_best;
+      st.hprim[slot] = T.best;
+      st.hface[slot] = T.face;
+      active = false;
+    }
+  }
+  unsigned long long v = visits, pt = ptests, r = rays;
+  for (int off = 32; off > 0; off >>= 1) {
+    v += __shfl_down(v, off);
+    pt += __shfl_down(pt, off);
+    r += __shfl_down(r, off);
+  }
+  if (lane == 0) {
+    DCounters* cs = P.counters + ((blockIdx.x * (kExtendThreads / kWave) + tid / kWave) % kCounterSlots);
+    atomicAdd(&cs->node_visits, v);
+    atomicAdd(&cs->prim_tests, pt);
+    atomicAdd(&cs->segments, r);  // ray_color loop iterations that traced a ray (render.rs:31)
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// wf_shade (+ path regeneration)
+// ------------------------------------------------------------------------------------------
+// The texture a material reads, resolved down to its leaf (checker.rs:27-37 picks odd/even by the
+// sign of a sine product).  Returns the leaf index.
+__device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
+  for (;;) {
+    const DTex& t = S.texs[ti];
+    if (t.kind != RT_TEX_CHECKER) return ti;
+    double sines = checker_sines(t.scale, p.x, p.y, p.z);
+    ti = (sines < 0.0) ? t.odd : t.even;
+  }
+}
+
+// Value of a solid leaf (solid.rs:17-21) or an image leaf (image_texture.rs:34-56); the image's u, v
+// come from the hit record, computed only here (prim_record<true>).
+__device__ __forceinline__ v3 leaf_value(const DScene& S, int ti, const DPrim& pr, int face, v3 o, v3 d, double t) {
+  const DTex& tx = S.texs[ti];
+  if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);
+  Hit h;
+  prim_record<true>(pr, face, o, d, t, h);
+  const DImage im = S.images[tx.table];
+  double uu = (h.u > 0.0) ? ((h.u < 1.0) ? h.u : 1.0) : 0.0;
+  double vv = 1.0 - ((h.v > 0.0) ? ((h.v < 1.0) ? h.v : 1.0) : 0.0);
+  uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
+  uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
+  const uint8_t* px = S.texels + im.offset + ((size_t)iy * (size_t)im.width + ix) * 3;
+  const double cs = 1.0 / 255.0;
+  return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
+}
+
+// One lane per slot; the grid covers the slots exactly in whole waves (n_slots % 64 == 0), and the
+// wave of slot group g = slots [64 g, 64 g + 64) owns that group's unit window and texture queue.
+__global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
+  const DScene& S = P.scene;
+  const DCamera& C = P.cam;
+  const DWork& W = P.work;
+  const WfState& st = P.st;
+  const uint64_t seed = W.seed;
+  const unsigned long long pix_per_chunk = (unsigned long long)W.n_tiles_rank * kTilePixels;
+  const int lane = __lane_id();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = i / kWave;
+  const bool valid = i < P.n_slots;
+  const int slot = (int)i;
+  unsigned n_samp = 0;
+
+  // wf_extend of this round is done with its slot cursors: zero them for the next round
+  if (blockIdx.x == 0 && threadIdx.x < kWfQueues) P.it->fetch[threadIdx.x][0] = 0;
+
+  uint8_t state = valid ? st.state[slot] : kSlotRetired;
+  bool defer = false;
+  int defer_kind = 0, defer_tex = 0;
+  double defer_scale = 0.0;
+  v3 hp = V(0, 0, 0);
+
+  // 1. shade the traced segment: render.rs:31-45
+  if (state == kSlotAlive) {
+    v3 o = V(st.ox[slot], st.oy[slot], st.oz[slot]);
+    v3 d = V(st.dx[slot], st.dy[slot], st.dz[slot]);
+    v3 att = V(st.ax[slot], st.ay[slot], st.az[slot]);
+    v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
+    Rng rng{st.pixel[slot], st.sample[slot], st.draw[slot], st.c2[slot], st.c3[slot]};
+    const int prim = st.hprim[slot];
+    bool alive;
+    if (prim >= 0) {
+      const DPrim pr = S.prims[prim];
+      const int face = st.hface[slot];
+      const double t = st.ht[slot];
+      Hit h;
+      prim_record<false>(pr, face, o, d, t, h);
+      hp = h.point;
+      const DMat m = S.mats[pr.material];
+      if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
+        double ratio = h.front_face ? (1.0 / m.param) : m.param;
+        v3 ud = unit(d);
+        double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
+        double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+        bool refl = ratio * sin_theta > 1.0;
+        if (!refl) refl = reflectance(cos_theta, ratio) > rng_next(rng, seed);  // drawn only if not TIR
+        o = h.point;
+        d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
+        alive = true;
+      } else if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
+        v3 r = random_in_unit_sphere(rng, seed);
+        v3 reflected = reflect(unit(d), h.normal);
+        o = h.point;
+        d = reflected + scale(r, m.param);
+        att = hmul(att, V(m.albedo[0], m.albedo[1], m.albedo[2]));
+        alive = true;
+      } else {
+        // Lambertian / FairyLight / DiffuseLight: the albedo texture
+        const int leaf = resolve_texture(S, m.tex, h.point);
+        const bool perlin = S.texs[leaf].kind == RT_TEX_PERLIN;
+        v3 a = perlin ? V(0, 0, 0) : leaf_value(S, leaf, pr, face, o, d, t);
+        if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
+          if (perlin) {
+            defer = true;
+            defer_kind = kDeferDiffuse;
+          } else {
+            em = em + hmul(att, a);
+          }
+          alive = false;
+        } else {  // lambertian.rs:21-37 / lighting.rs:42-66
+          if (m.kind == RT_MAT_FAIRY_LIGHT) {
+            double s = dot(h.normal, scale(d, -1.0));
+            if (perlin) {
+              defer_scale = s / len(d);
+            } else {
+              em = em + hmul(att, scale(a, s / len(d)));
+              a = unit(a);
+            }
+          }
+          v3 r = random_in_unit_sphere(rng, seed);
+          v3 sc = h.normal + unit(r);
+          if (near_zero(sc)) sc = h.normal;
+          o = h.point;
+          d = sc;
+          if (perlin) {
+            defer = true;
+            defer_kind = (m.kind == RT_MAT_FAIRY_LIGHT) ? kDeferFairy : kDeferLambertian;
+          } else {
+            att = hmul(att, a);
+          }
+          alive = true;
+        }
+        defer_tex = leaf;
+      }
+    } else {
+      em = em + hmul(att, sky(S, d));  // skybox/mod.rs:18-25
+      alive = false;
+    }
+    if (alive) {
+      const int dl = st.depth[slot] - 1;
+      st.depth[slot] = dl;
+      alive = dl > 0;
+    }
+    st.draw[slot] = rng.draw;
+    st.c2[slot] = rng.c2;
+    st.c3[slot] = rng.c3;
+    st.ax[slot] = att.x; st.ay[slot] = att.y; st.az[slot] = att.z;
+    st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
+    if (alive) {
+      st.ox[slot] = o.x; st.oy[slot] = o.y; st.oz[slot] = o.z;
+      st.dx[slot] = d.x; st.dy[slot] = d.y; st.dz[slot] = d.z;
+    } else {
+      // the path is finished; a deferred emission must land before its radiance is summed
+      state = defer ? kSlotEnded : kSlotIdle;
+      if (!defer) {
+        st.sx[slot] += em.x;  // c += ray_color(...)  (render.rs:66)
+        st.sy[slot] += em.y;
+        st.sz[slot] += em.z;
+      }
+    }
+  } else if (state == kSlotEnded) {
+    st.sx[slot] += st.ex[slot];
+    st.sy[slot] += st.ey[slot];
+    st.sz[slot] += st.ez[slot];
+    state = kSlotIdle;
+  }
+
+  // 2. deferred texture entry, compacted within the group (evaluated by wf_texture)
+  {
+    const unsigned long long md = __ballot(defer);
+    const unsigned q = g * kWave + (unsigned)__popcll(md & wf_lanemask_lt());
+    if (defer) {
+      P.tq.slot[q] = slot;
+      P.tq.tex[q] = defer_tex;
+      P.tq.kind[q] = defer_kind;
+      P.tq.px[q] = hp.x;
+      P.tq.py[q] = hp.y;
+      P.tq.pz[q] = hp.z;
+      P.tq.scale[q] = defer_scale;
+    }
+    if (lane == 0 && valid) P.tq.count[g] = (uint32_t)__popcll(md);
+  }
+
+  // 3. regeneration: a slot between paths starts its unit's next sample, or publishes the unit's
+  //    in-order sum (*buf_c = c, render.rs:68) and takes the next unit
+  uint32_t pix = kNoUnit;
+  int s_next = 0, s_end = 0;
+  const bool regen = state == kSlotIdle;
+  if (regen) {
+    pix = st.pixel[slot];
+    s_next = st.s_next[slot];
+    s_end = st.s_end[slot];
+    if (pix != kNoUnit && s_next >= s_end) {
+      double* dst = P.partial + st.part[slot] * 3;
+      dst[0] = st.sx[slot];
+      dst[1] = st.sy[slot];
+      dst[2] = st.sz[slot];
+      pix = kNoUnit;
+    }
+  }
+  const bool need_unit = regen && pix == kNoUnit;
+  const unsigned long long mneed = __ballot(need_unit);
+  bool retire = false;
+  if (mneed) {
+    // the group's window of units (one 64-unit refill per atomic, like the megakernel's waves)
+    unsigned long long wn, we;
+    if (P.first) {
+      wn = (unsigned long long)g * kWave;
+      we = wn + kWave;
+    } else {
+      wn = P.win[2 * g];
+      we = P.win[2 * g + 1];
+    }
+    const unsigned long long k = __popcll(mneed), rank = __popcll(mneed & wf_lanemask_lt());
+    const unsigned long long avail = we - wn;
+    unsigned long long idx;
+    if (avail >= k) {
+      idx = wn + rank;
+      wn += k;
+    } else {
+      unsigned long long nb = 0;
+      if (lane == 0) nb = (unsigned long long)P.n_slots + atomicAdd(P.unit_counter, (unsigned long long)kWave);
+      nb = __shfl(nb, 0);
+      idx = (rank < avail) ? (wn + rank) : (nb + (rank - avail));
+      wn = nb + (k - avail);
+      we = nb + kWave;
+    }
+    if (lane == 0) {
+      P.win[2 * g] = wn;
+      P.win[2 * g + 1] = we;
+    }
+    if (need_unit) {
+      if (idx < W.n_units) {
+        unsigned long long per_tile = (unsigned long long)W.n_chunks * kTilePixels;
+        unsigned long long lt = idx / per_tile;
+        unsigned long long rem = idx - lt * per_tile;
+        int chunk = (int)(rem / kTilePixels);
+        int lp = (int)(rem % kTilePixels);
+        unsigned long long gt = lt * (unsigned long long)W.tile_world + (unsigned long long)W.tile_rank;
+        int tx = (int)(gt % (unsigned long long)W.tiles_x), ty = W.ty0 + (int)(gt / (unsigned long long)W.tiles_x);
+        int ppx = tx * kTile + (lp % kTile), ppy = ty * kTile + (lp / kTile);
+        if (ppx < C.width && ppy < C.height) {
+          pix = (uint32_t)ppy * (uint32_t)C.width + (uint32_t)ppx;
+          s_next = chunk * W.chunk;
+          s_end = min(W.samples, s_next + W.chunk);
+          st.part[slot] = (unsigned long long)chunk * pix_per_chunk + lt * kTilePixels + (unsigned long long)lp;
+          st.sx[slot] = 0.0;
+          st.sy[slot] = 0.0;
+          st.sz[slot] = 0.0;
+          if (W.max_depth == 0) {  // ray_color returns black without drawing (render.rs:30)
+            n_samp += (unsigned)(s_end - s_next);
+            s_next = s_end;
+          }
+        }
+        // (a unit outside the image is skipped: the slot asks again next round)
+      } else {
+        state = kSlotRetired;
+        retire = true;
+      }
+    }
+  }
+  if (state == kSlotIdle && pix != kNoUnit && s_next < s_end) {  // render.rs:60-65
+    const int ppx = (int)(pix % (uint32_t)C.width), ppy = (int)(pix / (uint32_t)C.width);
+    Rng rng{pix, (uint32_t)s_next, 0u, 0u, 0u};
+    double jx = (double)ppx + rng_next(rng, seed);
+    double jy = (double)ppy + rng_next(rng, seed);
+    v3 o, d;
+    camera_ray(C, rng, seed, jx, jy, o, d);
+    st.ox[slot] = o.x; st.oy[slot] = o.y; st.oz[slot] = o.z;
+    st.dx[slot] = d.x; st.dy[slot] = d.y; st.dz[slot] = d.z;
+    st.ax[slot] = 1.0; st.ay[slot] = 1.0; st.az[slot] = 1.0;
+    st.ex[slot] = 0.0; st.ey[slot] = 0.0; st.ez[slot] = 0.0;
+    st.sample[slot] = rng.sample;
+    st.draw[slot] = rng.draw;
+    st.c2[slot] = rng.c2;
+    st.c3[slot] = rng.c3;
+    st.depth[slot] = W.max_depth;
+    ++s_next;
+    ++n_samp;
+    state = kSlotAlive;
+  }
+  if (valid && regen) {
+    st.pixel[slot] = pix;
+    st.s_next[slot] = s_next;
+    st.s_end[slot] = s_end;
+  }
+  if (valid) st.state[slot] = state;
+
+  // retirements (termination test on the host) and the samples counter: one atomic per wave/block
+  const unsigned long long mr = __ballot(retire);
+  if (mr && lane == 0) atomicAdd(P.retired, (unsigned)__popcll(mr));
+  __shared__ unsigned red[kGridThreads / kWave];
+  unsigned ns = n_samp;
+  for (int off = 32; off > 0; off >>= 1) ns += __shfl_down(ns, off);
+  if (lane == 0) red[threadIdx.x / kWave] = ns;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long tot = 0;
+    for (int w = 0; w < kGridThreads / kWave; ++w) tot += red[w];
+    if (tot) atomicAdd(&P.counters[blockIdx.x % kCounterSlots].samples, tot);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// wf_texture: deferred Perlin texture values; wave g evaluates group g's compacted entries
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kGridThreads) void wf_texture(WfParams P) {
+  const DScene& S = P.scene;
+  const WfState& st = P.st;
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = i / kWave;
+  if (i >= P.n_slots) return;
+  const uint32_t n = P.tq.count[g];
+  if ((uint32_t)__lane_id() >= n) return;
+  const int slot = P.tq.slot[i];
+  const DTex& t = S.texs[P.tq.tex[i]];
+  const v3 p = V(P.tq.px[i], P.tq.py[i], P.tq.pz[i]);
+  const double nz = marble(S.perlin + t.table, t.scale, p);  // perlin/mod.rs:162-183
+  v3 a = V(nz, nz, nz);
+  v3 att = V(st.ax[slot], st.ay[slot], st.az[slot]);
+  const int kind = P.tq.kind[i];
+  if (kind == kDeferLambertian) {
+    att = hmul(att, a);
+  } else if (kind == kDeferFairy) {  // emitted (lighting.rs:59-66) before the scatter attenuation
+    v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
+    em = em + hmul(att, scale(a, P.tq.scale[i]));
+    st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
+    att = hmul(att, unit(a));
+  } else {  // DiffuseLight
+    v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
+    em = em + hmul(att, a);
+    st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
+  }
+  st.ax[slot] = att.x; st.ay[slot] = att.y; st.az[slot] = att.z;
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launch helpers (called from rt_api.cpp)
+// ------------------------------------------------------------------------------------------
+size_t wf_extend_lds(int n_lds_nodes, int stack_depth) {
+  return (size_t)n_lds_nodes * sizeof(DNode) + (size_t)stack_depth * kExtendThreads * 8;
+}
+
+int wf_extend_threads() { return kExtendThreads; }
+
+static int wf_mode(const DScene& S) {
+  return S.n_lds_nodes >= S.n_nodes ? kNodesLds : (S.n_lds_nodes == 0 ? kNodesGlobal : kNodesMixed);
+}
+
+hipError_t wf_prepare(const DScene& S, int* extend_blocks_per_cu) {
+  const int lds = (int)wf_extend_lds(S.n_lds_nodes, S.stack_depth);
+  hipError_t e = hipSuccess;
+  switch (wf_mode(S)) {
+    case kNodesLds:
+      e = hipFuncSetAttribute((const void*)wf_extend<kNodesLds>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend<kNodesLds>, kExtendThreads, lds);
+      break;
+    case kNodesGlobal:
+      e = hipFuncSetAttribute((const void*)wf_extend<kNodesGlobal>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend<kNodesGlobal>, kExtendThreads, lds);
+      break;
+    default:
+      e = hipFuncSetAttribute((const void*)wf_extend<kNodesMixed>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend<kNodesMixed>, kExtendThreads, lds);
+  }
+  return e;
+}
+
+int wf_grid_threads() { return kGridThreads; }
+
+// One round = wf_launch_extend -> wf_launch_shade -> wf_launch_texture; `P.it` points at the
+// round's zeroed counters.
+hipError_t wf_launch_extend(const WfParams& P, int extend_blocks, hipStream_t s) {
+  const size_t lds = wf_extend_lds(P.scene.n_lds_nodes, P.scene.stack_depth);
+  switch (wf_mode(P.scene)) {
+    case kNodesLds: hipLaunchKernelGGL(wf_extend<kNodesLds>, dim3(extend_blocks), dim3(kExtendThreads), lds, s, P); break;
+    case kNodesGlobal: hipLaunchKernelGGL(wf_extend<kNodesGlobal>, dim3(extend_blocks), dim3(kExtendThreads), lds, s, P); break;
+    default: hipLaunchKernelGGL(wf_extend<kNodesMixed>, dim3(extend_blocks), dim3(kExtendThreads), lds, s, P);
+  }
+  return hipGetLastError();
+}
+
+hipError_t wf_launch_shade(const WfParams& P, int grid_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(wf_shade, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+  return hipGetLastError();
+}
+
+hipError_t wf_launch_texture(const WfParams& P, int grid_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(wf_texture, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+  return hipGetLastError();
+}
+
+// First iteration: every slot is Idle -> wf_shade alone assigns units and generates camera rays.
+hipError_t wf_start(const WfParams& P, int grid_blocks, hipStream_t s) {
+  WfParams Q = P;
+  Q.first = 1;
+  hipLaunchKernelGGL(wf_shade, dim3(grid_blocks), dim3(kGridThreads), 0, s, Q);
+  return hipGetLastError();
+}
+
+}  // namespace rt

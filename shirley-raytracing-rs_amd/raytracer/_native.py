@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_DIR = os.path.join(_PKG_ROOT, "lib")
+# SHIRLEY_LIB_DIR selects an alternative in-tree build (A/B experiments); default: <pkg>/lib
+LIB_DIR = os.environ.get("SHIRLEY_LIB_DIR") or os.path.join(_PKG_ROOT, "lib")
 BIN_DIR = os.path.join(_PKG_ROOT, "bin")
 
 RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_OOM, RT_E_UNSUPPORTED = 0, 1, 2, 3, 4
@@ -18,6 +19,8 @@ RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_LAMBERTIAN, RT_MAT_DIFFUSE_LIGHT, RT_MAT
 RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_IMAGE = range(4)
 RT_SKY_ABOVE, RT_SKY_FLAT, RT_SKY_NONE = range(3)
 RT_BVH_REFERENCE, RT_BVH_SAH = 0, 1
+RT_BVH_NODES_GLOBAL, RT_BVH_NODES_HALF_LDS, RT_BVH_NODES_LDS = 0x100, 0x200, 0x400
+RT_ENGINE_AUTO, RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_TIMING = 0, 1, 2, 0x10
 
 _d3 = C.c_double * 3
 _d6 = C.c_double * 6
@@ -64,7 +67,7 @@ class rt_camera(C.Structure):
 class rt_render_params(C.Structure):
     _fields_ = [("samples", C.c_int32), ("max_depth", C.c_int32), ("seed", C.c_uint64),
                 ("tile_rank", C.c_int32), ("tile_world", C.c_int32), ("sample_chunk", C.c_int32),
-                ("reserved", C.c_int32)]
+                ("engine", C.c_int32)]
 
 
 class rt_scene_stats(C.Structure):
@@ -74,7 +77,9 @@ class rt_scene_stats(C.Structure):
 
 class rt_counters(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
-                ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double), ("reduce_ms", C.c_double)]
+                ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double), ("reduce_ms", C.c_double),
+                ("engine", C.c_int32), ("iterations", C.c_int32), ("slots", C.c_uint64),
+                ("extend_ms", C.c_double), ("shade_ms", C.c_double), ("texture_ms", C.c_double)]
 
 
 class rt_bvh_node(C.Structure):

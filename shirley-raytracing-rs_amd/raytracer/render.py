@@ -29,11 +29,16 @@ class RenderSettings:
     sample_chunk: int = 0
     tile_rank: int = 0
     tile_world: int = 1
+    engine: str = "auto"   # auto | megakernel | wavefront
+    timing: bool = False   # per-launch HIP-event timing of the wavefront kernels (rt_counters *_ms)
+
+    ENGINES = {"auto": N.RT_ENGINE_AUTO, "megakernel": N.RT_ENGINE_MEGAKERNEL, "wavefront": N.RT_ENGINE_WAVEFRONT}
 
     def params(self) -> N.rt_render_params:
         p = N.rt_render_params()
         p.samples, p.max_depth, p.seed = int(self.samples), int(self.max_reflect), int(self.seed)
         p.tile_rank, p.tile_world, p.sample_chunk = int(self.tile_rank), int(self.tile_world), int(self.sample_chunk)
+        p.engine = self.ENGINES[self.engine] | (N.RT_ENGINE_TIMING if self.timing else 0)
         return p
 
 
@@ -60,8 +65,11 @@ class Device:
     def handle(self):
         return self._h
 
-    def upload(self, scene: Scene, bvh: str = "reference") -> "Device":
+    def upload(self, scene: Scene, bvh: str = "reference", nodes: str = "auto") -> "Device":
+        """rt_scene_upload; `nodes` = auto | global | half-lds | lds (BVH node placement, tests/tuning)."""
         builder = {"reference": N.RT_BVH_REFERENCE, "sah": N.RT_BVH_SAH}[bvh]
+        builder |= {"auto": 0, "global": N.RT_BVH_NODES_GLOBAL, "half-lds": N.RT_BVH_NODES_HALF_LDS,
+                    "lds": N.RT_BVH_NODES_LDS}[nodes]
         _check(self._h, N.rt_lib().rt_scene_upload(self._h, scene.desc_ptr, builder))
         self.scene = scene
         return self

@@ -9,6 +9,8 @@ at exactly the same t, which changes one whole path.  The test therefore demands
   * >= 95 % of pixel channels bit-identical (sample_chunk = spp: in-order sums like render.rs:58-69),
   * every channel within TOL = 1e-10 * spp absolute of the oracle, except at most 0.1 % of pixels
     (a flipped path changes one sample by up to the path's radiance).
+Both trace engines (RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT) run the same binary64 code on the same
+counter-RNG streams, so their frames must be bit-identical to each other.
 """
 import ctypes as C
 
@@ -21,6 +23,7 @@ import raytracer as rt
 pytestmark = pytest.mark.gpu
 
 SEED = 0x5EED
+ENGINES = ["megakernel", "wavefront"]
 
 
 def check_parity(gpu_img, ora_img, spp, frac_exact=0.95, frac_outlier=0.001):
@@ -44,25 +47,93 @@ def test_render_matches_oracle(gpu, name, width, aspect):
     scene = rt.SceneBuilder.builtin(name, SEED).finalize(SEED)
     cam = rt.scene_camera(name, width, aspect)
     gpu.upload(scene)
-    img = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp))
     ora, ocnt = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED))
-    check_parity(img, ora, spp)
-    cnt = gpu.counters()
-    assert cnt.samples == cam.image_width * cam.image_height * spp == ocnt.samples
-    # segment counts follow from the (identical) paths
-    assert abs(int(cnt.segments) - int(ocnt.segments)) <= 0.001 * ocnt.segments
+    imgs = {}
+    for engine in ENGINES:
+        img = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp,
+                                                engine=engine))
+        check_parity(img, ora, spp)
+        cnt = gpu.counters()
+        assert cnt.engine == {"megakernel": 1, "wavefront": 2}[engine]
+        assert cnt.samples == cam.image_width * cam.image_height * spp == ocnt.samples
+        # segment counts follow from the (identical) paths
+        assert abs(int(cnt.segments) - int(ocnt.segments)) <= 0.001 * ocnt.segments
+        imgs[engine] = img
+    assert np.array_equal(imgs["megakernel"], imgs["wavefront"])
 
 
-def test_sah_tree_same_image(gpu):
+@pytest.mark.parametrize("slots", ["64", "4096"])
+def test_wavefront_small_slot_pool(gpu, slots, monkeypatch):
+    """Far fewer path slots than work units: every slot regenerates many paths and takes many
+    units (render.rs:58-69 per slot); chunked sums and all counters equal the megakernel's."""
+    monkeypatch.setenv("SHIRLEY_WF_SLOTS", slots)
+    spp = 6
+    for name, width, aspect in [("perlin", 40, "std16x9"), ("cornell", 24, "square")]:
+        scene = rt.SceneBuilder.builtin(name, SEED).finalize(SEED)
+        cam = rt.scene_camera(name, width, aspect)
+        gpu.upload(scene)
+        a = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=2, engine="megakernel"))
+        ca = gpu.counters()
+        b = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=2, engine="wavefront"))
+        cb = gpu.counters()
+        assert np.array_equal(a, b)
+        assert 64 <= cb.slots <= int(slots) and cb.iterations > 1
+        assert (ca.samples, ca.segments, ca.node_visits, ca.prim_tests) == \
+            (cb.samples, cb.segments, cb.node_visits, cb.prim_tests)
+
+
+def test_wavefront_timing_counters(gpu):
+    """Per-launch event timing; the perlin scene has deferred texture work (a scene without Perlin
+    textures skips the wf_texture launch)."""
+    scene = rt.SceneBuilder.builtin("perlin", SEED).finalize(SEED)
+    cam = rt.scene_camera("perlin", 64, "std16x9")
+    gpu.upload(scene, "sah")
+    a = gpu.render(cam, rt.RenderSettings(samples=4, seed=SEED, engine="wavefront", timing=True))
+    c = gpu.counters()
+    assert c.engine == 2 and c.iterations > 4
+    assert c.extend_ms > 0 and c.shade_ms > 0 and c.texture_ms > 0
+    assert c.extend_ms + c.shade_ms + c.texture_ms <= c.kernel_ms * 1.05
+    b = gpu.render(cam, rt.RenderSettings(samples=4, seed=SEED, engine="wavefront"))
+    assert np.array_equal(a, b)
+    assert gpu.counters().extend_ms == 0.0
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_sah_tree_same_image(gpu, engine):
     spp = 4
     scene = rt.scenes.random_scene(SEED).finalize(SEED)
     cam = rt.default_camera(64, "std16x9")
-    s = rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp)
+    s = rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp)
     a = gpu.upload(scene, "reference").render(cam, s)
     b = gpu.upload(scene, "sah").render(cam, s)
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED))
     check_parity(a, ora, spp)
     check_parity(b, ora, spp)
+
+
+@pytest.mark.parametrize("nodes", ["lds", "half-lds"])
+@pytest.mark.parametrize("engine", ENGINES)
+def test_node_placements_same_image(gpu, engine, nodes):
+    """BVH nodes through L1/L2 (default), all in LDS, or split: the same pixels."""
+    spp = 3
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    cam = rt.default_camera(40, "std16x9")
+    s = rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp)
+    a = gpu.upload(scene, "sah").render(cam, s)
+    b = gpu.upload(scene, "sah", nodes).render(cam, s)
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("engine", ENGINES)
+def test_large_scene_mixed_lds_matches_oracle(gpu, engine):
+    """1,728 spheres (gen_spheres side 6): a deeper BVH, both builders, against the oracle."""
+    spp = 2
+    scene = rt.scenes.gen_spheres(0xDEADBEEF, 6).finalize(1)
+    cam = rt.scene_camera("spheres", 40, "std16x9")
+    for bvh in ("reference", "sah"):
+        img = gpu.upload(scene, bvh).render(cam, rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp))
+        ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED))
+        check_parity(img, ora, spp)
 
 
 def test_hit_queries_match_oracle(gpu):
@@ -110,12 +181,13 @@ def test_bbox_tree_unit_cases_on_gpu(gpu):
         assert got.object == want, (sph[:2], ray)
 
 
-def test_scanlines_equal_full_frame(gpu):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_scanlines_equal_full_frame(gpu, engine):
     spp = 4
     scene = rt.scenes.random_scene(SEED).finalize(SEED)
     cam = rt.default_camera(40, "std16x9")  # 40 x 22: rows not a multiple of 8
     gpu.upload(scene)
-    s = rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp)
+    s = rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp)
     full = gpu.render(cam, s)
     part = gpu.render_scanlines(cam, s, 5, 17)
     assert np.array_equal(part, full[5:17])
@@ -127,7 +199,8 @@ def test_scanlines_equal_full_frame(gpu):
     check_parity(part[4:5], row[None], spp, frac_exact=0.9, frac_outlier=0.05)
 
 
-def test_tiles_gather_unpack_equals_full_frame(gpu):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_tiles_gather_unpack_equals_full_frame(gpu, engine):
     """The multi-GPU data path on one device: each rank's packed tiles, concatenated like a
     gather, then unpacked, equal the single-rank frame bit for bit."""
     import torch
@@ -135,11 +208,11 @@ def test_tiles_gather_unpack_equals_full_frame(gpu):
     scene = rt.scenes.random_scene(SEED).finalize(SEED)
     cam = rt.default_camera(52, "std16x9")  # 52 x 29: partial tiles on both axes
     gpu.upload(scene)
-    full = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
+    full = gpu.render(cam, rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp))
     n_total, max_tiles = rt.tile_layout(cam, world)
     gathered = torch.zeros((world, max_tiles, 64, 3), dtype=torch.float64, device="cuda")
     for r in range(world):
-        gpu.render_tiles_device(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp, tile_rank=r,
+        gpu.render_tiles_device(cam, rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp, tile_rank=r,
                                                        tile_world=world), gathered[r].data_ptr())
     gpu.synchronize()
     accum = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.float64, device="cuda")
@@ -148,40 +221,43 @@ def test_tiles_gather_unpack_equals_full_frame(gpu):
     assert np.array_equal(accum.cpu().numpy(), full)
 
 
-def test_chunked_sums_close_to_in_order(gpu):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_chunked_sums_close_to_in_order(gpu, engine):
     spp = 24
     scene = rt.scenes.random_scene(SEED).finalize(SEED)
     cam = rt.default_camera(32, "std16x9")
     gpu.upload(scene)
-    a = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
-    b = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=5))
+    a = gpu.render(cam, rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp))
+    b = gpu.render(cam, rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=5))
     assert np.allclose(a, b, rtol=1e-12, atol=1e-12)
 
 
-def test_edge_cases(gpu):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_edge_cases(gpu, engine):
     scene = rt.scenes.random_scene(SEED).finalize(SEED)
     gpu.upload(scene)
     cam = rt.default_camera(8, "square")
     # samples == 0 renders one sample (main.rs:75-80)
-    z = gpu.render(cam, rt.RenderSettings(samples=0, seed=SEED))
-    one = gpu.render(cam, rt.RenderSettings(samples=1, seed=SEED))
+    z = gpu.render(cam, rt.RenderSettings(engine=engine, samples=0, seed=SEED))
+    one = gpu.render(cam, rt.RenderSettings(engine=engine, samples=1, seed=SEED))
     assert np.array_equal(z, one)
     # max_depth == 0 -> black (ray_color's loop never runs)
-    assert not gpu.render(cam, rt.RenderSettings(samples=2, max_reflect=0, seed=SEED)).any()
+    assert not gpu.render(cam, rt.RenderSettings(engine=engine, samples=2, max_reflect=0, seed=SEED)).any()
     # empty scene -> pure sky, equal to the oracle
     empty = O.SphereScene([])
     rt.Device.upload(gpu, type("S", (), {"desc_ptr": empty.desc_ptr})())
-    sky = gpu.render(cam, rt.RenderSettings(samples=2, seed=SEED, sample_chunk=2))
+    sky = gpu.render(cam, rt.RenderSettings(engine=engine, samples=2, seed=SEED, sample_chunk=2))
     ora, _ = O.OracleScene(empty).render(cam, O.params(2, 50, SEED))
     assert np.array_equal(sky, ora)
     # bad arguments fail loudly with a message
     with pytest.raises(rt.RtError):
-        gpu.render(cam, rt.RenderSettings(samples=-1))
+        gpu.render(cam, rt.RenderSettings(engine=engine, samples=-1))
     with pytest.raises(rt.RtError):
-        gpu.render_scanlines(cam, rt.RenderSettings(samples=1), 5, 100)
+        gpu.render_scanlines(cam, rt.RenderSettings(engine=engine, samples=1), 5, 100)
 
 
-def test_full_size_rows_match_oracle(gpu):
+@pytest.mark.parametrize("engine", ENGINES)
+def test_full_size_rows_match_oracle(gpu, engine):
     """BASELINE config 2 geometry (1200x800, random_scene) at reduced spp: two full rows against the
     oracle, plus the size-independent property full-frame row == rt_render_scanlines row."""
     spp = 6
@@ -189,7 +265,7 @@ def test_full_size_rows_match_oracle(gpu):
     cam = rt.default_camera(1200, "std3x2")
     assert (cam.image_width, cam.image_height) == (1200, 800)
     gpu.upload(scene)
-    s = rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp)
+    s = rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp)
     full = gpu.render(cam, s)
     rows = gpu.render_scanlines(cam, s, 200, 202)
     assert np.array_equal(rows, full[200:202])
