@@ -121,7 +121,8 @@ def main():
         c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
         kernel_ms.append(c.kernel_ms)
         segments.append(c.segments)
-        laps.append((c.engine, c.iterations, c.slots, c.extend_ms, c.shade_ms, c.texture_ms))
+        laps.append((c.engine, c.iterations, c.slots, c.extend_ms, c.shade_ms, c.texture_ms, c.node_visits,
+                     c.prim_tests))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -158,7 +159,9 @@ def main():
                    "slots": laps[-1][2],
                    "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
                                        "texture": round(laps[-1][5], 3)} if args.timing else None,
-                   "segments_per_sample": round(seg / (W * H * args.spp / world), 4) if world == 1 else None},
+                   "segments_per_sample": round(seg / (W * H * args.spp / world), 4) if world == 1 else None,
+                   "node_tests_per_segment": round(laps[-1][6] / max(seg, 1), 3),
+                   "prim_tests_per_segment": round(laps[-1][7] / max(seg, 1), 3)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),

@@ -446,27 +446,32 @@ __device__ __forceinline__ int32_t sat_i32(double x) {
   return (int32_t)x;
 }
 
-// perlin/mod.rs:87-109 + interp 40-63
-__device__ __noinline__ double perlin_noise(const DPerlin* T, v3 p) {
+// perlin/mod.rs:87-109 + interp 40-63.  The six permutation entries and then the eight gradient
+// vectors are fetched as independent loads (the corner loop of the reference serialises four
+// dependent loads per corner); the accumulation runs in the reference's (di, dj, dk) order with
+// its exact expressions, so the value is bit-identical.
+__device__ __forceinline__ double perlin_noise_inl(const DPerlin* T, v3 p) {
   double xf = floor(p.x), yf = floor(p.y), zf = floor(p.z);
   double u = p.x - xf, v = p.y - yf, w = p.z - zf;
   uint32_t i = (uint32_t)sat_i32(xf), j = (uint32_t)sat_i32(yf), k = (uint32_t)sat_i32(zf);
   double uu = u * u * (3.0 - 2.0 * u);
   double vv = v * v * (3.0 - 2.0 * v);
   double ww = w * w * (3.0 - 2.0 * w);
+  const int px[2] = {T->perm_x[i & 0xFF], T->perm_x[(i + 1) & 0xFF]};
+  const int py[2] = {T->perm_y[j & 0xFF], T->perm_y[(j + 1) & 0xFF]};
+  const int pz[2] = {T->perm_z[k & 0xFF], T->perm_z[(k + 1) & 0xFF]};
   double accum = 0.0;
-#pragma unroll 1
+#pragma unroll
   for (int di = 0; di < 2; ++di) {
-    double fi = (double)di;
-    int px = T->perm_x[(i + di) & 0xFF];
-#pragma unroll 1
+    const double fi = (double)di;
+#pragma unroll
     for (int dj = 0; dj < 2; ++dj) {
-      double fj = (double)dj;
-      int pxy = px ^ T->perm_y[(j + dj) & 0xFF];
-#pragma unroll 1
+      const double fj = (double)dj;
+      const int pxy = px[di] ^ py[dj];
+#pragma unroll
       for (int dk = 0; dk < 2; ++dk) {
-        double fk = (double)dk;
-        int idx = pxy ^ T->perm_z[(k + dk) & 0xFF];
+        const double fk = (double)dk;
+        const int idx = pxy ^ pz[dk];
         v3 c = V(T->ranfloat[idx][0], T->ranfloat[idx][1], T->ranfloat[idx][2]);
         v3 weight = V(u - fi, v - fj, w - fk);
         accum += (fi * uu + (1.0 - fi) * (1.0 - uu)) * (fj * vv + (1.0 - fj) * (1.0 - vv)) *
@@ -477,20 +482,31 @@ __device__ __noinline__ double perlin_noise(const DPerlin* T, v3 p) {
   return accum;
 }
 
+__device__ __noinline__ double perlin_noise(const DPerlin* T, v3 p) { return perlin_noise_inl(T, p); }
+
 // perlin/mod.rs:162-183 NoiseTexture::value ("marble"): 0.5 (1 + sin(scale p.z + 10 turb(p, 7)));
-// the x/y terms of the reference's dot with (0,0,1) contribute exactly 0.
-__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) {
+// the x/y terms of the reference's dot with (0,0,1) contribute exactly 0.  NOISE = the octave's
+// noise function (out-of-line in the megakernel to hold its registers, inline in wf_texture).
+template <double (*NOISE)(const DPerlin*, v3)>
+__device__ __forceinline__ double marble_impl(const DPerlin* T, double sc, v3 p) {
   double accum = 0.0;
   v3 tp = p;
   double weight = 1.0;
+#pragma unroll 1
   for (int i = 0; i < 7; ++i) {  // turbulence, perlin/mod.rs:111-124
-    accum += weight * perlin_noise(T, tp);
+    accum += weight * NOISE(T, tp);
     weight *= 0.5;
     tp = scale(tp, 2.0);
   }
   double turb = 10.0 * fabs(accum);
   double total_noise = sin(sc * p.z + turb);
   return 0.5 * (1.0 + total_noise);
+}
+
+__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) { return marble_impl<perlin_noise>(T, sc, p); }
+
+__device__ __forceinline__ double marble_inl(const DPerlin* T, double sc, v3 p) {
+  return marble_impl<perlin_noise_inl>(T, sc, p);
 }
 
 // checker.rs:28-30

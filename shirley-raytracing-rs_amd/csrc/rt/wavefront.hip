@@ -443,7 +443,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_texture(WfParams P) {
   const int slot = P.tq.slot[i];
   const DTex& t = S.texs[P.tq.tex[i]];
   const v3 p = V(P.tq.px[i], P.tq.py[i], P.tq.pz[i]);
-  const double nz = marble(S.perlin + t.table, t.scale, p);  // perlin/mod.rs:162-183
+  const double nz = marble_inl(S.perlin + t.table, t.scale, p);  // perlin/mod.rs:162-183
   v3 a = V(nz, nz, nz);
   v3 att = V(st.ax[slot], st.ay[slot], st.az[slot]);
   const int kind = P.tq.kind[i];
