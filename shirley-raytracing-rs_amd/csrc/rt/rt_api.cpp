@@ -18,9 +18,9 @@
 #include "rt_layout.h"
 
 namespace rt {
-size_t trace_lds_bytes(int n_lds_nodes, int stack_depth);
-hipError_t trace_occupancy(const DScene& S, int* blocks_per_cu);
-hipError_t launch_trace(const KParams& p, int blocks, hipStream_t stream);
+size_t trace_lds_bytes(int n_lds_nodes, int stack_depth, int threads);
+hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
+hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
                          int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
 hipError_t launch_unpack(const double* gathered, int world, int max_tiles, int n_tiles_total, int tiles_x, int width,
@@ -56,6 +56,7 @@ struct rt_ctx {
   DevBuf nodes, prims, mats, texs, perlin, images, texels;
   rt_scene_stats stats{};
   int blocks_per_cu = 0;
+  int mk_threads = kTraceThreads;  // megakernel block size (kTraceThreadsWide: whole BVH in LDS)
   // wavefront engine: the scene with its LDS node count sized for the extend block
   DScene wf_scene{};
   int wf_blocks_per_cu = 0;
@@ -489,7 +490,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   int chunk = p->sample_chunk;
   if (chunk == 0 && engine == RT_ENGINE_WAVEFRONT) chunk = kWfDefaultChunk;
   if (chunk == 0) {
-    long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * kTraceThreads;
+    long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
     long long want_units = 16 * lanes;
     long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
     n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
@@ -532,7 +533,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   } else {
     const int blocks = std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
     HIP_TRY(c, hipEventRecord(c->ev[0], s));
-    if (n_pix > 0) HIP_TRY(c, launch_trace(kp, blocks, s));
+    if (n_pix > 0) HIP_TRY(c, launch_trace(kp, blocks, c->mk_threads, s));
     HIP_TRY(c, hipEventRecord(c->ev[1], s));
   }
   if (n_pix > 0)
@@ -694,20 +695,26 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.stack_depth = depth + 2;  // ordered traversal holds at most one deferred child per branch level
   S.sky = d->sky;
   for (int k = 0; k < 3; ++k) S.sky_color[k] = d->sky_color[k];
-  // LDS of one block: the traversal stacks, then (placement flags) a copy of the BVH's top levels
-  long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
-  if (stack_bytes > kLdsBytes)
-    return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
+  // LDS of one block: the traversal stacks, then a copy of (the top levels of) the BVH.
+  // Default: the whole BVH in LDS with one kTraceThreadsWide block per CU when it fits beside the
+  // stacks (MI355X: 160 KiB per CU), else kTraceThreads blocks reading nodes through L1/L2.
   auto lds_nodes_for = [&](long long stack) -> int32_t {
     long long room = std::min<long long>((kLdsBytes - stack) / (long long)sizeof(DNode), (long long)nodes.size());
     if (placement & RT_BVH_NODES_LDS) return (int32_t)room;
     if (placement & RT_BVH_NODES_HALF_LDS) return (int32_t)std::min<long long>(room, (long long)nodes.size() / 2);
-    return 0;  // default: nodes read through L1/L2
+    if (const char* e = getenv("SHIRLEY_LDS_NODES")) return (int32_t)std::min<long long>(room, atoll(e));  // tuning
+    return 0;  // nodes read through L1/L2
   };
-  S.n_lds_nodes = lds_nodes_for(stack_bytes);
+  const long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
+  const long long wide_bytes = (long long)S.stack_depth * kTraceThreadsWide * 8 + (long long)nodes.size() * sizeof(DNode);
+  if (stack_bytes > kLdsBytes)
+    return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
+  const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS);
+  c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
+  S.n_lds_nodes = wide ? (int32_t)nodes.size() : lds_nodes_for(stack_bytes);
 
   int bpc = 0;
-  HIP_TRY(c, trace_occupancy(S, &bpc));
+  HIP_TRY(c, trace_occupancy(S, c->mk_threads, &bpc));
   if (bpc < 1) return fail(c, RT_E_UNSUPPORTED, "trace kernel does not fit on a CU (LDS %lld B)", stack_bytes);
   c->blocks_per_cu = bpc;
 
@@ -852,6 +859,16 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
     out->node_visits += k.node_visits;
     out->prim_tests += k.prim_tests;
   }
+#ifdef RT_PHASE_TIMING
+  {
+    double ph[3] = {0, 0, 0};
+    for (const DCounters& k : dc)
+      for (int i = 0; i < 3; ++i) ph[i] += (double)k.pad[i];
+    const double tot = ph[0] + ph[1] + ph[2];
+    fprintf(stderr, "[phase] regen %.3f trav %.3f shade %.3f (wave-cycles %.4g)\n", ph[0] / tot, ph[1] / tot,
+            ph[2] / tot, tot);
+  }
+#endif
   float a = 0.f, b = 0.f;
   HIP_TRY(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
   HIP_TRY(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));

@@ -514,29 +514,62 @@ __device__ __noinline__ double checker_sines(double s, double x, double y, doubl
   return sin(s * x) * sin(s * y) * sin(s * z);
 }
 
-__device__ __forceinline__ v3 texture_value(const DScene& S, int ti, double u, double v, v3 p) {
+// The texture a material reads, resolved down to its leaf (checker.rs:27-37 picks odd/even by the
+// sign of a sine product).  Returns the leaf index.
+__device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
   for (;;) {
     const DTex& t = S.texs[ti];
-    if (t.kind == RT_TEX_SOLID) return V(t.color[0], t.color[1], t.color[2]);  // solid.rs:17-21
-    if (t.kind == RT_TEX_CHECKER) {                                             // checker.rs:27-37
-      double sines = checker_sines(t.scale, p.x, p.y, p.z);
-      ti = (sines < 0.0) ? t.odd : t.even;
-      continue;
-    }
-    if (t.kind == RT_TEX_PERLIN) {
-      double n = marble(S.perlin + t.table, t.scale, p);
-      return V(n, n, n);
-    }
-    // image_texture.rs:34-56: clamp, flip v, truncate, /255
-    const DImage im = S.images[t.table];
-    double uu = (u > 0.0) ? ((u < 1.0) ? u : 1.0) : 0.0;
-    double vv = 1.0 - ((v > 0.0) ? ((v < 1.0) ? v : 1.0) : 0.0);
-    uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
-    uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
-    const uint8_t* px = S.texels + im.offset + ((size_t)iy * (size_t)im.width + ix) * 3;
-    const double cs = 1.0 / 255.0;
-    return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
+    if (t.kind != RT_TEX_CHECKER) return ti;
+    double sines = checker_sines(t.scale, p.x, p.y, p.z);
+    ti = (sines < 0.0) ? t.odd : t.even;
   }
+}
+
+// image_texture.rs:34-56: clamp, flip v, truncate, /255.
+__device__ __forceinline__ v3 image_texel(const DScene& S, const DTex& tx, double u, double v) {
+  const DImage im = S.images[tx.table];
+  double uu = (u > 0.0) ? ((u < 1.0) ? u : 1.0) : 0.0;
+  double vv = 1.0 - ((v > 0.0) ? ((v < 1.0) ? v : 1.0) : 0.0);
+  uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
+  uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
+  const uint8_t* px = S.texels + im.offset + ((size_t)iy * (size_t)im.width + ix) * 3;
+  const double cs = 1.0 / 255.0;
+  return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
+}
+
+// u, v of a hit record built without them (prim_record<false>), from the record itself: a sphere's
+// outward normal is the record's normal un-flipped (negation is exact), and a rect's o1 + t d1 is
+// exactly the record's point component (x*y == y*x); the formulas are then prim_record's.
+__device__ __forceinline__ UV hit_uv(const DPrim& pr, int face, const Hit& h) {
+  if (pr.kind == kPrimSphere) {
+    const v3 n = h.front_face ? h.normal : scale(h.normal, -1.0);
+    return sphere_uv(n.x, n.y, n.z);
+  }
+  const double* b = pr.p;
+  int kind = pr.kind;
+  double q0 = b[0], q1 = b[1], q2 = b[2], q3 = b[3];
+  if (kind == kPrimBox) {
+    if (face < 2) { q0 = b[0]; q1 = b[3]; q2 = b[1]; q3 = b[4]; kind = kPrimRectXY; }
+    else if (face < 4) { q0 = b[1]; q1 = b[4]; q2 = b[2]; q3 = b[5]; kind = kPrimRectYZ; }
+    else { q0 = b[0]; q1 = b[3]; q2 = b[2]; q3 = b[5]; kind = kPrimRectXZ; }
+  }
+  const double a1 = (kind == kPrimRectYZ) ? h.point.y : h.point.x;
+  const double a2 = (kind == kPrimRectXY) ? h.point.y : h.point.z;
+  return UV{(a1 - q0) / (q1 - q0), (a2 - q2) / (q3 - q2)};
+}
+
+// Texture value at a hit (texture.rs Texture::value): checker resolved by the hit point, Perlin
+// marble by the hit point, solid directly, image by u, v (computed only for an image leaf).
+__device__ __forceinline__ v3 texture_value(const DScene& S, int ti, int prim, int face, const Hit& h) {
+  const int leaf = resolve_texture(S, ti, h.point);
+  const DTex& tx = S.texs[leaf];
+  if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);  // solid.rs:17-21
+  if (tx.kind == RT_TEX_PERLIN) {
+    double n = marble(S.perlin + tx.table, tx.scale, h.point);
+    return V(n, n, n);
+  }
+  const UV uv = hit_uv(S.prims[prim], face, h);
+  return image_texel(S, tx, uv.u, uv.v);
 }
 
 // dielectric.rs:15-19
@@ -560,10 +593,12 @@ __device__ __forceinline__ v3 sky(const DScene& S, v3 d) {
 // One ray_color loop iteration after the hit (render.rs:31-40): emitted, then scatter.
 // Returns false when the path ends (material absorbed).  Metal, Lambertian and FairyLight all draw
 // random_in_unit_sphere (metal.rs:32, lambertian.rs:23 via random_unit_vector); it has one call site.
+// The hit record comes without u, v (prim_record<false>); (prim, face, t) let an image texture
+// rebuild them.
 __device__ __forceinline__ bool shade(const DScene& S, const DMat& m, Rng& rng, uint64_t seed, v3& o, v3& d,
-                                      const Hit& h, v3& att, v3& em) {
+                                      const Hit& h, int prim, int face, v3& att, v3& em) {
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
-    v3 e = texture_value(S, m.tex, h.u, h.v, h.point);
+    v3 e = texture_value(S, m.tex, prim, face, h);
     em = em + hmul(att, e);
     return false;
   }
@@ -587,7 +622,7 @@ __device__ __forceinline__ bool shade(const DScene& S, const DMat& m, Rng& rng, 
     return true;
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
-  v3 a = texture_value(S, m.tex, h.u, h.v, h.point);
+  v3 a = texture_value(S, m.tex, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
     double s = dot(h.normal, scale(d, -1.0));
     em = em + hmul(att, scale(a, s / len(d)));

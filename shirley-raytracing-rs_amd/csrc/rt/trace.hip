@@ -30,14 +30,16 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
   return (size_t)n_lds_nodes * sizeof(DNode) + (size_t)stack_depth * stride * 8;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kTraceThreads, 3) void trace_kernel(KParams P) {
+// THREADS = kTraceThreads (several blocks per CU, 3 waves/SIMD) or kTraceThreadsWide (one block per
+// CU whose LDS holds the whole BVH next to the stacks); the register budget is 168 VGPRs either way.
+template <int THREADS, int MODE>
+__global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
   DNode* lds_nodes = reinterpret_cast<DNode*>(lds_raw);
   unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes * sizeof(DNode);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
-  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth * kTraceThreads * 4) + tid;
+  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth * THREADS * 4) + tid;
   stage_nodes<MODE>(P.scene, lds_nodes);
 
   const DScene& S = P.scene;
@@ -62,7 +64,13 @@ __global__ __launch_bounds__(kTraceThreads, 3) void trace_kernel(KParams P) {
   unsigned long long n_vis = 0, n_pt = 0;
   const unsigned long long pix_per_chunk = (unsigned long long)W.n_tiles_rank * kTilePixels;
 
+#ifdef RT_PHASE_TIMING
+  unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0;
+#endif
   for (;;) {
+#ifdef RT_PHASE_TIMING
+    const unsigned long long ph0 = clock64();
+#endif
     // 1. a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
     if (has_unit && !active && s_cur >= s_end) {
       double* dst = P.partial + part_index * 3;
@@ -134,18 +142,26 @@ __global__ __launch_bounds__(kTraceThreads, 3) void trace_kernel(KParams P) {
       continue;
     }
     // 4. one ray_color iteration (render.rs:30-46): closest hit, then emitted + scatter or sky
+#ifdef RT_PHASE_TIMING
+    const unsigned long long ph1 = clock64();
+    ph_regen += ph1 - ph0;
+#endif
     if (active) {
       ++n_seg;
       double t_best = __builtin_inf();
       int face = -1;
-      int prim = traverse<kTraceThreads, MODE>(S, lds_nodes, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
+      int prim = traverse<THREADS, MODE>(S, lds_nodes, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
+#ifdef RT_PHASE_TIMING
+      const unsigned long long ph2 = clock64();
+      ph_trav += ph2 - ph1;
+#endif
       bool alive;
       if (prim >= 0) {
         const DPrim pr = S.prims[prim];
         Hit h;
-        prim_record(pr, face, o, d, t_best, h);
+        prim_record<false>(pr, face, o, d, t_best, h);
         const DMat m = S.mats[pr.material];
-        alive = shade(S, m, rng, seed, o, d, h, att, em);
+        alive = shade(S, m, rng, seed, o, d, h, prim, face, att, em);
       } else {
         em = em + hmul(att, sky(S, d));
         alive = false;
@@ -155,6 +171,9 @@ __global__ __launch_bounds__(kTraceThreads, 3) void trace_kernel(KParams P) {
         sum = sum + em;  // c += ray_color(...)
         active = false;
       }
+#ifdef RT_PHASE_TIMING
+      ph_shade += clock64() - ph2;
+#endif
     }
     if (visits > (1u << 30)) { n_vis += visits; visits = 0; }
     if (ptests > (1u << 30)) { n_pt += ptests; ptests = 0; }
@@ -174,6 +193,11 @@ __global__ __launch_bounds__(kTraceThreads, 3) void trace_kernel(KParams P) {
     atomicAdd(&cs->samples, n_samp);
     atomicAdd(&cs->node_visits, n_vis);
     atomicAdd(&cs->prim_tests, n_pt);
+#ifdef RT_PHASE_TIMING
+    atomicAdd(&cs->pad[0], ph_regen);
+    atomicAdd(&cs->pad[1], ph_trav);
+    atomicAdd(&cs->pad[2], ph_shade);
+#endif
   }
 }
 
@@ -277,40 +301,56 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
-size_t trace_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kTraceThreads); }
+size_t trace_lds_bytes(int n_lds_nodes, int stack_depth, int threads) {
+  return lds_bytes(n_lds_nodes, stack_depth, threads);
+}
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 
 static int node_mode(const DScene& S) {
   return S.n_lds_nodes >= S.n_nodes ? kNodesLds : (S.n_lds_nodes == 0 ? kNodesGlobal : kNodesMixed);
 }
 
-template <int MODE>
+template <int THREADS, int MODE>
 static hipError_t occupancy_impl(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
-  hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)trace_lds_bytes(S.n_lds_nodes, S.stack_depth));
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes, S.stack_depth, THREADS);
+  hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)hit_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           (int)hit_lds_bytes(S.n_lds_nodes, S.stack_depth));
   if (e != hipSuccess) return e;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<MODE>, kTraceThreads,
-                                                       trace_lds_bytes(S.n_lds_nodes, S.stack_depth));
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<THREADS, MODE>, THREADS, lds);
 }
 
-hipError_t trace_occupancy(const DScene& S, int* blocks_per_cu) {
+// Kernel instances: the wide block only with the whole BVH in LDS.
+hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
+  if (threads == kTraceThreadsWide) {
+    if (node_mode(S) != kNodesLds) return hipErrorInvalidValue;
+    return occupancy_impl<kTraceThreadsWide, kNodesLds>(S, blocks_per_cu);
+  }
   switch (node_mode(S)) {
-    case kNodesLds: return occupancy_impl<kNodesLds>(S, blocks_per_cu);
-    case kNodesGlobal: return occupancy_impl<kNodesGlobal>(S, blocks_per_cu);
-    default: return occupancy_impl<kNodesMixed>(S, blocks_per_cu);
+    case kNodesLds: return occupancy_impl<kTraceThreads, kNodesLds>(S, blocks_per_cu);
+    case kNodesGlobal: return occupancy_impl<kTraceThreads, kNodesGlobal>(S, blocks_per_cu);
+    default: return occupancy_impl<kTraceThreads, kNodesMixed>(S, blocks_per_cu);
   }
 }
 
-hipError_t launch_trace(const KParams& p, int blocks, hipStream_t stream) {
-  size_t lds = trace_lds_bytes(p.scene.n_lds_nodes, p.scene.stack_depth);
+hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
+  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes, p.scene.stack_depth, threads);
+  if (threads == kTraceThreadsWide) {
+    hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
+    return hipGetLastError();
+  }
   switch (node_mode(p.scene)) {
-    case kNodesLds: hipLaunchKernelGGL(trace_kernel<kNodesLds>, dim3(blocks), dim3(kTraceThreads), lds, stream, p); break;
-    case kNodesGlobal: hipLaunchKernelGGL(trace_kernel<kNodesGlobal>, dim3(blocks), dim3(kTraceThreads), lds, stream, p); break;
-    default: hipLaunchKernelGGL(trace_kernel<kNodesMixed>, dim3(blocks), dim3(kTraceThreads), lds, stream, p);
+    case kNodesLds:
+      hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
+      break;
+    case kNodesGlobal:
+      hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesGlobal>), dim3(blocks), dim3(threads), lds, stream, p);
+      break;
+    default:
+      hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesMixed>), dim3(blocks), dim3(threads), lds, stream, p);
   }
   return hipGetLastError();
 }

@@ -135,34 +135,6 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
 // ------------------------------------------------------------------------------------------
 // wf_shade (+ path regeneration)
 // ------------------------------------------------------------------------------------------
-// The texture a material reads, resolved down to its leaf (checker.rs:27-37 picks odd/even by the
-// sign of a sine product).  Returns the leaf index.
-__device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
-  for (;;) {
-    const DTex& t = S.texs[ti];
-    if (t.kind != RT_TEX_CHECKER) return ti;
-    double sines = checker_sines(t.scale, p.x, p.y, p.z);
-    ti = (sines < 0.0) ? t.odd : t.even;
-  }
-}
-
-// Value of a solid leaf (solid.rs:17-21) or an image leaf (image_texture.rs:34-56); the image's u, v
-// come from the hit record, computed only here (prim_record<true>).
-__device__ __forceinline__ v3 leaf_value(const DScene& S, int ti, const DPrim& pr, int face, v3 o, v3 d, double t) {
-  const DTex& tx = S.texs[ti];
-  if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);
-  Hit h;
-  prim_record<true>(pr, face, o, d, t, h);
-  const DImage im = S.images[tx.table];
-  double uu = (h.u > 0.0) ? ((h.u < 1.0) ? h.u : 1.0) : 0.0;
-  double vv = 1.0 - ((h.v > 0.0) ? ((h.v < 1.0) ? h.v : 1.0) : 0.0);
-  uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
-  uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
-  const uint8_t* px = S.texels + im.offset + ((size_t)iy * (size_t)im.width + ix) * 3;
-  const double cs = 1.0 / 255.0;
-  return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
-}
-
 // One lane per slot; the grid covers the slots exactly in whole waves (n_slots % 64 == 0), and the
 // wave of slot group g = slots [64 g, 64 g + 64) owns that group's unit window and texture queue.
 __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
@@ -226,7 +198,16 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
         // Lambertian / FairyLight / DiffuseLight: the albedo texture
         const int leaf = resolve_texture(S, m.tex, h.point);
         const bool perlin = S.texs[leaf].kind == RT_TEX_PERLIN;
-        v3 a = perlin ? V(0, 0, 0) : leaf_value(S, leaf, pr, face, o, d, t);
+        v3 a = V(0, 0, 0);
+        if (!perlin) {
+          const DTex& tx = S.texs[leaf];
+          if (tx.kind == RT_TEX_SOLID) {
+            a = V(tx.color[0], tx.color[1], tx.color[2]);
+          } else {
+            const UV uv = hit_uv(pr, face, h);
+            a = image_texel(S, tx, uv.u, uv.v);
+          }
+        }
         if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
           if (perlin) {
             defer = true;

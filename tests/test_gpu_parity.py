@@ -111,7 +111,7 @@ def test_sah_tree_same_image(gpu, engine):
     check_parity(b, ora, spp)
 
 
-@pytest.mark.parametrize("nodes", ["lds", "half-lds"])
+@pytest.mark.parametrize("nodes", ["global", "lds", "half-lds"])
 @pytest.mark.parametrize("engine", ENGINES)
 def test_node_placements_same_image(gpu, engine, nodes):
     """BVH nodes through L1/L2 (default), all in LDS, or split: the same pixels."""
