@@ -53,7 +53,7 @@ struct rt_ctx {
   // scene
   bool have_scene = false;
   DScene scene{};
-  DevBuf nodes, prims, mats, texs, perlin, images, texels;
+  DevBuf nodes, nodes4, prims, mats, texs, perlin, images, texels;
   rt_scene_stats stats{};
   int blocks_per_cu = 0;
   int mk_threads = kTraceThreads;  // megakernel block size (kTraceThreadsWide: whole BVH in LDS)
@@ -251,6 +251,67 @@ void flatten(const BuiltTree& t, std::vector<DNode>& out) {
     out.push_back(DNode{});
     q.push_back({bn.lhs, idx, 0});
     q.push_back({bn.rhs, idx, 1});
+  }
+}
+
+// Collapse heuristic: half the surface area of a box (0 for an inverted or NaN box).
+double half_area(const Box& b) {
+  const double x = b.mx[0] - b.mn[0], y = b.mx[1] - b.mn[1], z = b.mx[2] - b.mn[2];
+  if (!(x >= 0.0 && y >= 0.0 && z >= 0.0)) return 0.0;
+  return x * y + y * z + z * x;
+}
+
+// BuiltTree -> 4-wide nodes for the megakernel: each node takes its two children and then, while
+// it has fewer than four, replaces its largest-area internal child by that child's two children
+// (order kept).  Boxes stay the reference's exact boxes.  `stack_bound` = the worst-case traversal
+// stack: the sum over a root path of (internal children - 1) per node (at most that many pushes).
+void flatten4(const BuiltTree& t, std::vector<DNode4>& out, int32_t& stack_bound) {
+  out.clear();
+  DNode4 top{};
+  for (int k = 0; k < 4; ++k) top.child[k] = kEmptyChild;
+  out.push_back(top);
+  stack_bound = 1;
+  if (t.root < 0) return;
+  auto internal = [&](int32_t n) { return t.nodes[n].leaf < 0; };
+  struct Item {
+    int32_t built;
+    int32_t parent;
+    int slot;
+    int32_t level;  // stack entries that can be live when this node is visited
+  };
+  std::vector<Item> q{{t.root, 0, 0, 0}};
+  for (size_t head = 0; head < q.size(); ++head) {
+    const Item it = q[head];
+    const BuildNode& bn = t.nodes[it.built];
+    box_to_node(bn.box, out[it.parent].box[it.slot]);
+    if (bn.leaf >= 0) {
+      out[it.parent].child[it.slot] = ~bn.leaf;
+      continue;
+    }
+    const int32_t idx = (int32_t)out.size();
+    out[it.parent].child[it.slot] = idx;
+    DNode4 nd{};
+    for (int k = 0; k < 4; ++k) nd.child[k] = kEmptyChild;
+    out.push_back(nd);
+    std::vector<int32_t> ch{bn.lhs, bn.rhs};
+    while (ch.size() < 4) {
+      int pick = -1;
+      double best = -1.0;
+      for (size_t i = 0; i < ch.size(); ++i)
+        if (internal(ch[i]) && half_area(t.nodes[ch[i]].box) > best) {
+          best = half_area(t.nodes[ch[i]].box);
+          pick = (int)i;
+        }
+      if (pick < 0) break;
+      const int32_t x = ch[pick];
+      ch[pick] = t.nodes[x].lhs;
+      ch.insert(ch.begin() + pick + 1, t.nodes[x].rhs);
+    }
+    int n_int = 0;
+    for (int32_t c : ch) n_int += internal(c) ? 1 : 0;
+    const int32_t level = it.level + std::max(0, n_int - 1);
+    stack_bound = std::max(stack_bound, level + 1);
+    for (size_t i = 0; i < ch.size(); ++i) q.push_back({ch[i], idx, (int)i, level});
   }
 }
 
@@ -591,7 +652,7 @@ int rt_destroy(rt_ctx* c) {
   if (!c) return RT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->nodes, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->partial,
+  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->partial,
                     &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters})
     release(*b);
   for (auto& e : c->ev)
@@ -620,6 +681,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   BuiltTree tree = build_tree(d, builder);
   std::vector<DNode> nodes;
   flatten(tree, nodes);
+  std::vector<DNode4> nodes4;
+  int32_t stack4 = 1;
+  flatten4(tree, nodes4, stack4);
   std::vector<DPrim> prims(std::max(1, d->n_objects));
   for (int i = 0; i < d->n_objects; ++i) {
     const rt_object& o = d->objects[i];
@@ -674,6 +738,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   if (texels.empty()) texels.resize(16);
 
   if ((st = upload(c, c->nodes, nodes.data(), nodes.size() * sizeof(DNode)))) return st;
+  if ((st = upload(c, c->nodes4, nodes4.data(), nodes4.size() * sizeof(DNode4)))) return st;
   if ((st = upload(c, c->prims, prims.data(), prims.size() * sizeof(DPrim)))) return st;
   if ((st = upload(c, c->mats, mats.data(), mats.size() * sizeof(DMat)))) return st;
   if ((st = upload(c, c->texs, texs.data(), texs.size() * sizeof(DTex)))) return st;
@@ -683,6 +748,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
 
   DScene& S = c->scene;
   S.nodes = static_cast<const DNode*>(c->nodes.p);
+  S.nodes4 = static_cast<const DNode4*>(c->nodes4.p);
+  S.n_nodes4 = (int32_t)nodes4.size();
+  S.stack_depth4 = stack4;
   S.prims = static_cast<const DPrim*>(c->prims.p);
   S.mats = static_cast<const DMat*>(c->mats.p);
   S.texs = static_cast<const DTex*>(c->texs.p);
@@ -696,22 +764,27 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.sky = d->sky;
   for (int k = 0; k < 3; ++k) S.sky_color[k] = d->sky_color[k];
   // LDS of one block: the traversal stacks, then a copy of (the top levels of) the BVH.
-  // Default: the whole BVH in LDS with one kTraceThreadsWide block per CU when it fits beside the
-  // stacks (MI355X: 160 KiB per CU), else kTraceThreads blocks reading nodes through L1/L2.
-  auto lds_nodes_for = [&](long long stack) -> int32_t {
-    long long room = std::min<long long>((kLdsBytes - stack) / (long long)sizeof(DNode), (long long)nodes.size());
+  // Megakernel (4-wide tree): the whole tree in LDS with one kTraceThreadsWide block per CU when it
+  // fits beside the stacks (MI355X: 160 KiB per CU), else kTraceThreads blocks reading nodes
+  // through L1/L2.  rt_scene_hit (2-wide tree): placement flags only.
+  auto lds_count = [&](long long stack, size_t node_bytes, size_t n) -> int32_t {
+    long long room = std::min<long long>((kLdsBytes - stack) / (long long)node_bytes, (long long)n);
     if (placement & RT_BVH_NODES_LDS) return (int32_t)room;
-    if (placement & RT_BVH_NODES_HALF_LDS) return (int32_t)std::min<long long>(room, (long long)nodes.size() / 2);
+    if (placement & RT_BVH_NODES_HALF_LDS) return (int32_t)std::min<long long>(room, (long long)n / 2);
     if (const char* e = getenv("SHIRLEY_LDS_NODES")) return (int32_t)std::min<long long>(room, atoll(e));  // tuning
     return 0;  // nodes read through L1/L2
   };
+  auto lds_nodes_for = [&](long long stack) { return lds_count(stack, sizeof(DNode), nodes.size()); };
   const long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
-  const long long wide_bytes = (long long)S.stack_depth * kTraceThreadsWide * 8 + (long long)nodes.size() * sizeof(DNode);
-  if (stack_bytes > kLdsBytes)
+  const long long stack4_bytes = (long long)S.stack_depth4 * kTraceThreads * 8;
+  const long long wide_bytes =
+      (long long)S.stack_depth4 * kTraceThreadsWide * 8 + (long long)nodes4.size() * sizeof(DNode4);
+  if (stack_bytes > kLdsBytes || stack4_bytes > kLdsBytes)
     return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
   const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS);
   c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
-  S.n_lds_nodes = wide ? (int32_t)nodes.size() : lds_nodes_for(stack_bytes);
+  S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
+  S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4), nodes4.size());
 
   int bpc = 0;
   HIP_TRY(c, trace_occupancy(S, c->mk_threads, &bpc));

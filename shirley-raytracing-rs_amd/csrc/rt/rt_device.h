@@ -277,7 +277,7 @@ struct Trav {
   v3 inv;         // 1/d per axis (aabb.rs:66 computes the same quotient per call)
   double a;       // |d|^2 (sphere.rs:31)
   double t_best;  // closest accepted t so far (t_max initially)
-  int best, face, node, sp;
+  int best, face, node, sp, steps;
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, v3 d, double t_max) {
@@ -288,6 +288,7 @@ __device__ __forceinline__ void trav_begin(Trav& T, v3 d, double t_max) {
   T.face = -1;
   T.node = 0;  // top node: child[0] = root
   T.sp = 0;
+  T.steps = 0;
 }
 
 // Node source by kernel instance: all nodes in LDS, all in HBM/L2, or the first n_lds_nodes (BFS
@@ -322,6 +323,7 @@ __device__ __forceinline__ void leaf_visit(const DScene& S, int prim, v3 o, v3 d
 template <int STRIDE, int MODE>
 __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_nodes, v3 o, v3 d, double t_min, Trav& T,
                                           int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
+  if (++T.steps > S.n_nodes) return true;  // defect guard: a traversal visits each node at most once
   const DNode& nd = fetch_node<MODE>(S, lds_nodes, T.node);
   const int c0 = nd.child[0], c1 = nd.child[1];
   double te0 = 0.0, te1 = 0.0;
@@ -375,7 +377,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
   int best = -1;
   int sp = 0;
   int node = 0;  // top node: child[0] = root
-  for (;;) {
+  for (int steps = 0; steps < S.n_nodes; ++steps) {  // bounded like traverse4
     const DNode& nd = fetch_node<MODE>(S, lds_nodes, node);
     const int c0 = nd.child[0], c1 = nd.child[1];
     double te0 = 0.0, te1 = 0.0;
@@ -423,6 +425,112 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
     node = next;
   }
   return best;
+}
+
+// ---- 4-wide traversal (megakernel) ----
+template <int MODE>
+__device__ __forceinline__ const DNode4& fetch_node4(const DScene& S, const DNode4* lds_nodes, int idx) {
+  if (MODE == kNodesLds) return lds_nodes[idx];
+  if (MODE == kNodesGlobal) return S.nodes4[idx];
+  return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : S.nodes4[idx];
+}
+
+// compare-exchange of (key, node) pairs: ascending key
+__device__ __forceinline__ void cas(double& ka, int& na, double& kb, int& nb) {
+  const bool sw = kb < ka;
+  const double k = sw ? kb : ka;
+  const int n = sw ? nb : na;
+  kb = sw ? ka : kb;
+  nb = sw ? na : nb;
+  ka = k;
+  na = n;
+}
+
+// Closest hit over the 4-wide tree: the child boxes of a node are tested with the reference's f64
+// hit2, hit leaf children are tested at once in child order (they can shrink t_best), hit internal
+// children are visited nearest-first (the others pushed with their entry t; a popped entry beyond
+// t_best is skipped).  The exact boxes make every pruning decision one the reference's traversal
+// would also take, so the closest hit is the reference's (up to exact ties in t).
+template <int STRIDE, int MODE>
+__device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_nodes, v3 o, v3 d, double t_min,
+                                         double& t_best, int& face_best, int* stk_node, float* stk_t,
+                                         unsigned& visits, unsigned& ptests) {
+  const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  const double a = len2(d);
+  int best = -1;
+  int sp = 0;
+  int node = 0;  // top node: child[0] = root
+  const double kInf = __builtin_inf();
+  // a tree traversal visits every node at most once: more steps than nodes can only be a defect,
+  // and ends the loop instead of hanging the wave
+  for (int steps = 0; steps < S.n_nodes4; ++steps) {
+    const DNode4& nd = fetch_node4<MODE>(S, lds_nodes, node);
+    int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
+    double k0 = kInf, k1 = kInf, k2 = kInf, k3 = kInf;
+    double te;
+    const bool h0 = (c0 != kEmptyChild) && slab(nd.box[0], o, inv, t_min, t_best, te);
+    if (h0) k0 = te;
+    const bool h1 = (c1 != kEmptyChild) && slab(nd.box[1], o, inv, t_min, t_best, te);
+    if (h1) k1 = te;
+    const bool h2 = (c2 != kEmptyChild) && slab(nd.box[2], o, inv, t_min, t_best, te);
+    if (h2) k2 = te;
+    const bool h3 = (c3 != kEmptyChild) && slab(nd.box[3], o, inv, t_min, t_best, te);
+    if (h3) k3 = te;
+    visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
+    // hit leaf children, in child order
+    unsigned lm = (h0 && c0 < 0 ? 1u : 0u) | (h1 && c1 < 0 ? 2u : 0u) | (h2 && c2 < 0 ? 4u : 0u) |
+                  (h3 && c3 < 0 ? 8u : 0u);
+#pragma unroll 1
+    while (lm) {
+      const int k = __builtin_ctz(lm);
+      lm &= lm - 1;
+      const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
+      const DPrim& pr = S.prims[leaf];
+      double t;
+      int f = -1;
+      ++ptests;
+      if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; }
+    }
+    // internal children nearest-first: leaves and misses sort last (key inf)
+    if (c0 < 0) k0 = kInf;
+    if (c1 < 0) k1 = kInf;
+    if (c2 < 0) k2 = kInf;
+    if (c3 < 0) k3 = kInf;
+    cas(k0, c0, k1, c1);
+    cas(k2, c2, k3, c3);
+    cas(k0, c0, k2, c2);
+    cas(k1, c1, k3, c3);
+    cas(k1, c1, k2, c2);
+    // a hit box has a finite entry t, so key < inf marks exactly the hit internal children (t_best
+    // itself may still be inf)
+    if (k3 < kInf && k3 <= t_best) { stk_node[sp * STRIDE] = c3; stk_t[sp * STRIDE] = __double2float_rd(k3); ++sp; }
+    if (k2 < kInf && k2 <= t_best) { stk_node[sp * STRIDE] = c2; stk_t[sp * STRIDE] = __double2float_rd(k2); ++sp; }
+    if (k1 < kInf && k1 <= t_best) { stk_node[sp * STRIDE] = c1; stk_t[sp * STRIDE] = __double2float_rd(k1); ++sp; }
+    if (k0 < kInf && k0 <= t_best) {
+      node = c0;
+    } else {
+      node = -1;
+      while (sp > 0) {
+        --sp;
+        if ((double)stk_t[sp * STRIDE] <= t_best) {
+          node = stk_node[sp * STRIDE];
+          break;
+        }
+      }
+      if (node < 0) break;
+    }
+  }
+  return best;
+}
+
+template <int MODE>
+__device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4* lds_nodes) {
+  if (MODE == kNodesGlobal) return;
+  const int4* src = reinterpret_cast<const int4*>(S.nodes4);
+  int4* dst = reinterpret_cast<int4*>(lds_nodes);
+  const int n16 = S.n_lds_nodes4 * (int)(sizeof(DNode4) / 16);
+  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
 }
 
 // Copy nodes [0, n_lds_nodes) into the block's LDS node cache (16-B coalesced loads).
@@ -503,7 +611,10 @@ __device__ __forceinline__ double marble_impl(const DPerlin* T, double sc, v3 p)
   return 0.5 * (1.0 + total_noise);
 }
 
-__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) { return marble_impl<perlin_noise>(T, sc, p); }
+#ifndef RT_MARBLE_NOISE
+#define RT_MARBLE_NOISE perlin_noise_inl  // octave noise inside the out-of-line marble (perlin_noise: a call per octave)
+#endif
+__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) { return marble_impl<RT_MARBLE_NOISE>(T, sc, p); }
 
 __device__ __forceinline__ double marble_inl(const DPerlin* T, double sc, v3 p) {
   return marble_impl<perlin_noise_inl>(T, sc, p);

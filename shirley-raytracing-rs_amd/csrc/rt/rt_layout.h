@@ -31,6 +31,14 @@ struct alignas(16) DNode {
 };
 static_assert(sizeof(DNode) == 112, "DNode layout");
 
+// 4-wide node of the collapsed tree used by the megakernel (fewer dependent node fetches per ray);
+// same exact f64 child boxes and child encoding as DNode.
+struct alignas(16) DNode4 {
+  double box[4][6];
+  int32_t child[4];
+};
+static_assert(sizeof(DNode4) == 208, "DNode4 layout");
+
 // Where a kernel instance reads BVH nodes from (template parameter of the traversal):
 enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2 };
 
@@ -83,6 +91,10 @@ struct DScene {
   int32_t n_nodes, n_prims;
   int32_t stack_depth;     // max stack entries a traversal can need
   int32_t n_lds_nodes;     // nodes [0, n_lds_nodes) are copied into LDS per block (BFS order: top levels)
+  const DNode4* nodes4;    // the same tree collapsed to 4-wide nodes (node 0 = top node)
+  int32_t n_nodes4;
+  int32_t stack_depth4;    // exact worst-case stack of the 4-wide traversal
+  int32_t n_lds_nodes4;    // 4-wide nodes [0, n_lds_nodes4) copied into LDS per megakernel block
   int32_t sky;
   double sky_color[3];
 };

@@ -36,11 +36,11 @@ template <int THREADS, int MODE>
 __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
-  DNode* lds_nodes = reinterpret_cast<DNode*>(lds_raw);
-  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes * sizeof(DNode);
+  DNode4* lds_nodes = reinterpret_cast<DNode4*>(lds_raw);
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
-  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth * THREADS * 4) + tid;
-  stage_nodes<MODE>(P.scene, lds_nodes);
+  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
+  stage_nodes4<MODE>(P.scene, lds_nodes);
 
   const DScene& S = P.scene;
   const DCamera& C = P.cam;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
       ++n_seg;
       double t_best = __builtin_inf();
       int face = -1;
-      int prim = traverse<THREADS, MODE>(S, lds_nodes, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
+      int prim = traverse4<THREADS, MODE>(S, lds_nodes, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
 #ifdef RT_PHASE_TIMING
       const unsigned long long ph2 = clock64();
       ph_trav += ph2 - ph1;
@@ -301,35 +301,48 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
-size_t trace_lds_bytes(int n_lds_nodes, int stack_depth, int threads) {
-  return lds_bytes(n_lds_nodes, stack_depth, threads);
+// megakernel block LDS: [n_lds_nodes4 x DNode4][stack_depth4 x threads int][stack_depth4 x threads float]
+size_t trace_lds_bytes(int n_lds_nodes4, int stack_depth4, int threads) {
+  return (size_t)n_lds_nodes4 * sizeof(DNode4) + (size_t)stack_depth4 * threads * 8;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 
 static int node_mode(const DScene& S) {
   return S.n_lds_nodes >= S.n_nodes ? kNodesLds : (S.n_lds_nodes == 0 ? kNodesGlobal : kNodesMixed);
 }
+static int node_mode4(const DScene& S) {
+  return S.n_lds_nodes4 >= S.n_nodes4 ? kNodesLds : (S.n_lds_nodes4 == 0 ? kNodesGlobal : kNodesMixed);
+}
 
 template <int THREADS, int MODE>
 static hipError_t occupancy_impl(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
-  const size_t lds = trace_lds_bytes(S.n_lds_nodes, S.stack_depth, THREADS);
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.stack_depth4, THREADS);
   hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)hit_kernel<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          (int)hit_lds_bytes(S.n_lds_nodes, S.stack_depth));
   if (e != hipSuccess) return e;
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<THREADS, MODE>, THREADS, lds);
 }
 
-// Kernel instances: the wide block only with the whole BVH in LDS.
+static hipError_t hit_prepare(const DScene& S) {
+  const int lds = (int)hit_lds_bytes(S.n_lds_nodes, S.stack_depth);
+  switch (node_mode(S)) {
+    case kNodesLds: return hipFuncSetAttribute((const void*)hit_kernel<kNodesLds>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    case kNodesGlobal: return hipFuncSetAttribute((const void*)hit_kernel<kNodesGlobal>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    default: return hipFuncSetAttribute((const void*)hit_kernel<kNodesMixed>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  }
+}
+
+// Kernel instances: the wide block only with the whole (4-wide) BVH in LDS.  Also prepares the
+// rt_scene_hit kernel for the scene.
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
+  hipError_t e = hit_prepare(S);
+  if (e != hipSuccess) return e;
   if (threads == kTraceThreadsWide) {
-    if (node_mode(S) != kNodesLds) return hipErrorInvalidValue;
+    if (node_mode4(S) != kNodesLds) return hipErrorInvalidValue;
     return occupancy_impl<kTraceThreadsWide, kNodesLds>(S, blocks_per_cu);
   }
-  switch (node_mode(S)) {
+  switch (node_mode4(S)) {
     case kNodesLds: return occupancy_impl<kTraceThreads, kNodesLds>(S, blocks_per_cu);
     case kNodesGlobal: return occupancy_impl<kTraceThreads, kNodesGlobal>(S, blocks_per_cu);
     default: return occupancy_impl<kTraceThreads, kNodesMixed>(S, blocks_per_cu);
@@ -337,12 +350,12 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
 }
 
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
-  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes, p.scene.stack_depth, threads);
+  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.stack_depth4, threads);
   if (threads == kTraceThreadsWide) {
     hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
     return hipGetLastError();
   }
-  switch (node_mode(p.scene)) {
+  switch (node_mode4(p.scene)) {
     case kNodesLds:
       hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
       break;

@@ -65,7 +65,7 @@ def test_render_matches_oracle(gpu, name, width, aspect):
 @pytest.mark.parametrize("slots", ["64", "4096"])
 def test_wavefront_small_slot_pool(gpu, slots, monkeypatch):
     """Far fewer path slots than work units: every slot regenerates many paths and takes many
-    units (render.rs:58-69 per slot); chunked sums and all counters equal the megakernel's."""
+    units (render.rs:58-69 per slot); chunked sums and path counters equal the megakernel's."""
     monkeypatch.setenv("SHIRLEY_WF_SLOTS", slots)
     spp = 6
     for name, width, aspect in [("perlin", 40, "std16x9"), ("cornell", 24, "square")]:
@@ -78,8 +78,9 @@ def test_wavefront_small_slot_pool(gpu, slots, monkeypatch):
         cb = gpu.counters()
         assert np.array_equal(a, b)
         assert 64 <= cb.slots <= int(slots) and cb.iterations > 1
-        assert (ca.samples, ca.segments, ca.node_visits, ca.prim_tests) == \
-            (cb.samples, cb.segments, cb.node_visits, cb.prim_tests)
+        # same paths: same samples and segments (node-test counts differ: the megakernel walks the
+        # 4-wide collapse of the tree, the wavefront engine the 2-wide tree)
+        assert (ca.samples, ca.segments) == (cb.samples, cb.segments)
 
 
 def test_wavefront_timing_counters(gpu):
