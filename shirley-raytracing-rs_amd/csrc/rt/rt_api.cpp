@@ -785,6 +785,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
   S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
   S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4), nodes4.size());
+  // primitives too, when they fit beside the wide block's tree and stacks (leaf tests from LDS)
+  const bool prims_lds = wide && wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) <= kLdsBytes &&
+                         !getenv("SHIRLEY_NO_LDS_PRIMS");
+  S.n_lds_prims = prims_lds ? d->n_objects : 0;
 
   int bpc = 0;
   HIP_TRY(c, trace_occupancy(S, c->mk_threads, &bpc));

@@ -430,7 +430,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
 // ---- 4-wide traversal (megakernel) ----
 template <int MODE>
 __device__ __forceinline__ const DNode4& fetch_node4(const DScene& S, const DNode4* lds_nodes, int idx) {
-  if (MODE == kNodesLds) return lds_nodes[idx];
+  if (MODE == kNodesLds || MODE == kSceneLds) return lds_nodes[idx];
   if (MODE == kNodesGlobal) return S.nodes4[idx];
   return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : S.nodes4[idx];
 }
@@ -452,7 +452,8 @@ __device__ __forceinline__ void cas(double& ka, int& na, double& kb, int& nb) {
 // t_best is skipped).  The exact boxes make every pruning decision one the reference's traversal
 // would also take, so the closest hit is the reference's (up to exact ties in t).
 template <int STRIDE, int MODE>
-__device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_nodes, v3 o, v3 d, double t_min,
+__device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
+                                         double t_min,
                                          double& t_best, int& face_best, int* stk_node, float* stk_t,
                                          unsigned& visits, unsigned& ptests) {
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
@@ -485,7 +486,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_node
       const int k = __builtin_ctz(lm);
       lm &= lm - 1;
       const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
-      const DPrim& pr = S.prims[leaf];
+      const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
       double t;
       int f = -1;
       ++ptests;
@@ -524,12 +525,18 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_node
 }
 
 template <int MODE>
-__device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4* lds_nodes) {
+__device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4* lds_nodes, DPrim* lds_prims) {
   if (MODE == kNodesGlobal) return;
   const int4* src = reinterpret_cast<const int4*>(S.nodes4);
   int4* dst = reinterpret_cast<int4*>(lds_nodes);
   const int n16 = S.n_lds_nodes4 * (int)(sizeof(DNode4) / 16);
   for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  if (MODE == kSceneLds) {
+    const int4* ps = reinterpret_cast<const int4*>(S.prims);
+    int4* pd = reinterpret_cast<int4*>(lds_prims);
+    const int p16 = S.n_lds_prims * (int)(sizeof(DPrim) / 16);
+    for (int i = threadIdx.x; i < p16; i += blockDim.x) pd[i] = ps[i];
+  }
   __syncthreads();
 }
 
@@ -625,14 +632,41 @@ __device__ __noinline__ double checker_sines(double s, double x, double y, doubl
   return sin(s * x) * sin(s * y) * sin(s * z);
 }
 
+// Sign of sin(y) for a double y, exactly: +1, -1 or 0 — or 2 when this fast path does not decide
+// (NaN, |y| < 1e-100, |y| > 3e6, or y within 1e-12 of a multiple of pi).  y is reduced by pi split in
+// three parts (P1, P2 with 33 significant bits, so k*P1 and k*P2 are exact for |k| < 2^20, and
+// y - k*P1 is exact by Sterbenz): r = y - k*pi to ~2^-100 absolute, and sin(y) = (-1)^k sin(r) with
+// |r| < pi, so sign(sin y) = (-1)^k sign(r).  Any faithful sin (glibc's, ocml's) has that sign.
+__device__ __forceinline__ int sin_sign(double y) {
+  if (y == 0.0) return 0;
+  const double ay = fabs(y);
+  if (!(ay >= 1e-100 && ay <= 3.0e6)) return 2;
+  const double P1 = 0x1.921fb54400000p+1, P2 = 0x1.0b4611a600000p-33, P3 = 0x1.3198a2e037073p-68;
+  const double k = rint(y * 0x1.45f306dc9c883p-2);  // y / pi
+  double r = fma(-k, P1, y);
+  r = fma(-k, P2, r);
+  r = fma(-k, P3, r);
+  if (fabs(r) < 1e-12) return 2;
+  const int sr = r > 0.0 ? 1 : -1;
+  return (((long long)k) & 1) ? -sr : sr;
+}
+
+// checker.rs:27-37 decides odd/even by `sin(s x) sin(s y) sin(s z) < 0.0` alone.  Each |factor| is
+// >= ~1e-100 on the fast path, so the product cannot underflow and its sign is the product of the
+// signs; anything the fast path cannot decide evaluates the reference's product.
+__device__ __forceinline__ bool checker_odd(double s, double x, double y, double z) {
+  const int a = sin_sign(s * x), b = sin_sign(s * y), c = sin_sign(s * z);
+  if (a == 2 || b == 2 || c == 2) return checker_sines(s, x, y, z) < 0.0;
+  return a * b * c < 0;
+}
+
 // The texture a material reads, resolved down to its leaf (checker.rs:27-37 picks odd/even by the
 // sign of a sine product).  Returns the leaf index.
 __device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
   for (;;) {
     const DTex& t = S.texs[ti];
     if (t.kind != RT_TEX_CHECKER) return ti;
-    double sines = checker_sines(t.scale, p.x, p.y, p.z);
-    ti = (sines < 0.0) ? t.odd : t.even;
+    ti = checker_odd(t.scale, p.x, p.y, p.z) ? t.odd : t.even;
   }
 }
 
@@ -683,11 +717,26 @@ __device__ __forceinline__ v3 texture_value(const DScene& S, int ti, int prim, i
   return image_texel(S, tx, uv.u, uv.v);
 }
 
-// dielectric.rs:15-19
+// x^5 for x in [0, 4] as a double-double product (x^2 and x^4 carried with their FMA-exact
+// low parts): within ~2^-100 relative of the exact value before the final rounding, i.e. correctly
+// rounded save for values within 2^-100 of a rounding boundary — as glibc's pow(x, 5.0) is (the
+// oracle's and the reference's libm).  Other x take pow().
+__device__ __forceinline__ double pow5(double x) {
+  if (!(x >= 0.0 && x <= 4.0)) return pow(x, 5.0);
+  const double x2 = x * x;
+  const double x2l = fma(x, x, -x2);
+  const double x4 = x2 * x2;
+  const double x4l = fma(x2, x2, -x4) + (2.0 * x2) * x2l;
+  const double x5 = x4 * x;
+  const double x5l = fma(x4, x, -x5) + x4l * x;
+  return x5 + x5l;
+}
+
+// dielectric.rs:15-19 (Schlick); only ever compared against a uniform draw (dielectric.rs:41)
 __device__ __noinline__ double reflectance(double cosine, double ref_idx) {
   double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
   r0 = r0 * r0;
-  return r0 + (1.0 - r0) * pow(1.0 - cosine, 5.0);
+  return r0 + (1.0 - r0) * pow5(1.0 - cosine);
 }
 
 // skybox/mod.rs:5-25

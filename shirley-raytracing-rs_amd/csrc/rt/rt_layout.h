@@ -40,7 +40,8 @@ struct alignas(16) DNode4 {
 static_assert(sizeof(DNode4) == 208, "DNode4 layout");
 
 // Where a kernel instance reads BVH nodes from (template parameter of the traversal):
-enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2 };
+enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2,
+             kSceneLds = 3 };  // kSceneLds: all nodes AND all primitives in LDS (megakernel, small scenes)
 
 // Primitive kinds (device-side, rect axis folded into the kind).
 enum : int32_t { kPrimSphere = 0, kPrimRectXY = 1, kPrimRectYZ = 2, kPrimRectXZ = 3, kPrimBox = 4 };
@@ -95,6 +96,7 @@ struct DScene {
   int32_t n_nodes4;
   int32_t stack_depth4;    // exact worst-case stack of the 4-wide traversal
   int32_t n_lds_nodes4;    // 4-wide nodes [0, n_lds_nodes4) copied into LDS per megakernel block
+  int32_t n_lds_prims;     // 0, or n_prims when the megakernel block also keeps the primitives in LDS
   int32_t sky;
   double sky_color[3];
 };

@@ -37,10 +37,12 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
   DNode4* lds_nodes = reinterpret_cast<DNode4*>(lds_raw);
-  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4));
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4) +
+                            (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) : 0);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
   float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
-  stage_nodes4<MODE>(P.scene, lds_nodes);
+  stage_nodes4<MODE>(P.scene, lds_nodes, lds_prims);
 
   const DScene& S = P.scene;
   const DCamera& C = P.cam;
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
       ++n_seg;
       double t_best = __builtin_inf();
       int face = -1;
-      int prim = traverse4<THREADS, MODE>(S, lds_nodes, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
+      int prim =
+          traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
 #ifdef RT_PHASE_TIMING
       const unsigned long long ph2 = clock64();
       ph_trav += ph2 - ph1;
@@ -301,9 +304,10 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
-// megakernel block LDS: [n_lds_nodes4 x DNode4][stack_depth4 x threads int][stack_depth4 x threads float]
-size_t trace_lds_bytes(int n_lds_nodes4, int stack_depth4, int threads) {
-  return (size_t)n_lds_nodes4 * sizeof(DNode4) + (size_t)stack_depth4 * threads * 8;
+// megakernel block LDS: [n_lds_nodes4 x DNode4][n_lds_prims x DPrim][stack_depth4 x threads int]
+// [stack_depth4 x threads float]
+size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int stack_depth4, int threads) {
+  return (size_t)n_lds_nodes4 * sizeof(DNode4) + (size_t)n_lds_prims * sizeof(DPrim) + (size_t)stack_depth4 * threads * 8;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 
@@ -317,7 +321,7 @@ static int node_mode4(const DScene& S) {
 template <int THREADS, int MODE>
 static hipError_t occupancy_impl(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
-  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.stack_depth4, THREADS);
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.n_lds_prims, S.stack_depth4, THREADS);
   hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -340,6 +344,7 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
   if (e != hipSuccess) return e;
   if (threads == kTraceThreadsWide) {
     if (node_mode4(S) != kNodesLds) return hipErrorInvalidValue;
+    if (S.n_lds_prims > 0) return occupancy_impl<kTraceThreadsWide, kSceneLds>(S, blocks_per_cu);
     return occupancy_impl<kTraceThreadsWide, kNodesLds>(S, blocks_per_cu);
   }
   switch (node_mode4(S)) {
@@ -350,9 +355,12 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
 }
 
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
-  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.stack_depth4, threads);
+  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.n_lds_prims, p.scene.stack_depth4, threads);
   if (threads == kTraceThreadsWide) {
-    hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
+    if (p.scene.n_lds_prims > 0)
+      hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kSceneLds>), dim3(blocks), dim3(threads), lds, stream, p);
+    else
+      hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
     return hipGetLastError();
   }
   switch (node_mode4(p.scene)) {
