@@ -944,6 +944,13 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
     const double tot = ph[0] + ph[1] + ph[2];
     fprintf(stderr, "[phase] regen %.3f trav %.3f shade %.3f (wave-cycles %.4g)\n", ph[0] / tot, ph[1] / tot,
             ph[2] / tot, tot);
+    double lane = 0, wave = 0;
+    for (const DCounters& k : dc) {
+      lane += (double)k.pad[3];
+      wave += (double)k.pad[4];
+    }
+    fprintf(stderr, "[phase] traversal lane steps %.4g, wave steps %.4g, SIMD utilisation %.3f\n", lane, wave,
+            lane / (64.0 * wave));
   }
 #endif
   float a = 0.f, b = 0.f;

@@ -113,22 +113,34 @@ __device__ __forceinline__ v3 random_in_unit_disk(Rng& r, uint64_t seed) {
 // ------------------------------------------------------------------------------------------
 // intersection (t only during traversal; the full hit record is rebuilt for the winner)
 // ------------------------------------------------------------------------------------------
-// aabb.rs:62-79 hit2; axes evaluated without early exit (t_min only grows, t_max only shrinks,
-// so the final `t_max <= t_min` test equals the reference's per-axis early return).
-__device__ __forceinline__ bool slab(const double* b, v3 o, v3 inv, double t_min, double t_max, double& t_enter) {
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    double iv = comp(inv, a);
-    double t0 = (b[a] - comp(o, a)) * iv;
-    double t1 = (b[a + 3] - comp(o, a)) * iv;
-    if (iv < 0.0) {
-      double tmp = t0;
-      t0 = t1;
-      t1 = tmp;
-    }
-    t_min = (t0 > t_min) ? t0 : t_min;
-    t_max = (t1 < t_max) ? t1 : t_max;
-  }
+// aabb.rs:62-79 hit2, per axis: t0 = (min - o) * inv, t1 = (max - o) * inv, swapped when inv < 0,
+// t_min = t0 > t_min ? t0 : t_min, t_max = t1 < t_max ? t1 : t_max, miss when t_max <= t_min
+// (evaluated without the per-axis early exit: t_min only grows and t_max only shrinks, so the final
+// test equals the reference's early return).
+// Implemented with the swap hoisted out: RaySigns = (1/d < 0) per axis, computed once per ray, to
+// pick the near / far plane, so t0, t1 are the values the reference's swap produces; the updates
+// `t0 > t_min ? t0 : t_min` and `t1 < t_max ? t1 : t_max` become v_max_f64 / v_min_f64, which also
+// return the non-NaN operand (a NaN t0 or t1 leaves the bound as the reference does), and differ
+// only on equal values (signed zeros), which no later comparison distinguishes.
+struct RaySigns {
+  bool x, y, z;
+};
+__device__ __forceinline__ RaySigns ray_signs(v3 inv) { return RaySigns{inv.x < 0.0, inv.y < 0.0, inv.z < 0.0}; }
+
+__device__ __forceinline__ bool slab_axis(double lo, double hi, bool neg, double o, double iv, double& t_min,
+                                          double& t_max) {
+  const double pn = neg ? hi : lo, pf = neg ? lo : hi;
+  const double t0 = (pn - o) * iv, t1 = (pf - o) * iv;
+  t_min = fmax(t0, t_min);
+  t_max = fmin(t1, t_max);
+  return true;
+}
+
+__device__ __forceinline__ bool slab_s(const double* b, v3 o, v3 inv, RaySigns ns, double t_min, double t_max,
+                                       double& t_enter) {
+  slab_axis(b[0], b[3], ns.x, o.x, inv.x, t_min, t_max);
+  slab_axis(b[1], b[4], ns.y, o.y, inv.y, t_min, t_max);
+  slab_axis(b[2], b[5], ns.z, o.z, inv.z, t_min, t_max);
   t_enter = t_min;
   return !(t_max <= t_min);
 }
@@ -277,6 +289,7 @@ __device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 
 // Traversal state of one ray.
 struct Trav {
   v3 inv;         // 1/d per axis (aabb.rs:66 computes the same quotient per call)
+  RaySigns ns;    // 1/d < 0 per axis
   double a;       // |d|^2 (sphere.rs:31)
   double t_best;  // closest accepted t so far (t_max initially)
   int best, face, node, sp, steps;
@@ -284,6 +297,7 @@ struct Trav {
 
 __device__ __forceinline__ void trav_begin(Trav& T, v3 d, double t_max) {
   T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  T.ns = ray_signs(T.inv);
   T.a = len2(d);
   T.t_best = t_max;
   T.best = -1;
@@ -329,8 +343,8 @@ __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_node
   const DNode& nd = fetch_node<MODE>(S, lds_nodes, T.node);
   const int c0 = nd.child[0], c1 = nd.child[1];
   double te0 = 0.0, te1 = 0.0;
-  bool h0 = (c0 != kEmptyChild) && slab(nd.box[0], o, T.inv, t_min, T.t_best, te0);
-  bool h1 = (c1 != kEmptyChild) && slab(nd.box[1], o, T.inv, t_min, T.t_best, te1);
+  bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, T.inv, T.ns, t_min, T.t_best, te0);
+  bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, T.inv, T.ns, t_min, T.t_best, te1);
   visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
   // leaf children (one primitive each)
   if (h0 && c0 < 0) {
@@ -375,6 +389,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
                                         double& t_best, int& face_best, int* stk_node, float* stk_t,
                                         unsigned& visits, unsigned& ptests) {
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  const RaySigns ns = ray_signs(inv);
   const double a = len2(d);
   int best = -1;
   int sp = 0;
@@ -383,8 +398,8 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
     const DNode& nd = fetch_node<MODE>(S, lds_nodes, node);
     const int c0 = nd.child[0], c1 = nd.child[1];
     double te0 = 0.0, te1 = 0.0;
-    bool h0 = (c0 != kEmptyChild) && slab(nd.box[0], o, inv, t_min, t_best, te0);
-    bool h1 = (c1 != kEmptyChild) && slab(nd.box[1], o, inv, t_min, t_best, te1);
+    bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, inv, ns, t_min, t_best, te0);
+    bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, inv, ns, t_min, t_best, te1);
     visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
     if (h0 && c0 < 0) {
       const DPrim& pr = S.prims[~c0];
@@ -430,6 +445,10 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
 }
 
 // ---- 4-wide traversal (megakernel) ----
+#ifdef RT_PHASE_TIMING
+// per-lane step counter of the instrumented build (a register of the calling kernel)
+#define g_trav_lane_steps trav_lane_steps_ref
+#endif
 template <int MODE>
 __device__ __forceinline__ const DNode4& fetch_node4(const DScene& S, const DNode4* lds_nodes, int idx) {
   if (MODE == kNodesLds || MODE == kSceneLds) return lds_nodes[idx];
@@ -457,8 +476,13 @@ template <int STRIDE, int MODE>
 __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                          double t_min,
                                          double& t_best, int& face_best, int* stk_node, float* stk_t,
-                                         unsigned& visits, unsigned& ptests) {
+                                         unsigned& visits, unsigned& ptests
+#ifdef RT_PHASE_TIMING
+                                         , unsigned long long& trav_lane_steps_ref
+#endif
+                                         ) {
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  const RaySigns ns = ray_signs(inv);
   const double a = len2(d);
   int best = -1;
   int sp = 0;
@@ -467,17 +491,20 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_node
   // a tree traversal visits every node at most once: more steps than nodes can only be a defect,
   // and ends the loop instead of hanging the wave
   for (int steps = 0; steps < S.n_nodes4; ++steps) {
+#ifdef RT_PHASE_TIMING
+    ++g_trav_lane_steps;
+#endif
     const DNode4& nd = fetch_node4<MODE>(S, lds_nodes, node);
     int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
     double k0 = kInf, k1 = kInf, k2 = kInf, k3 = kInf;
     double te;
-    const bool h0 = (c0 != kEmptyChild) && slab(nd.box[0], o, inv, t_min, t_best, te);
+    const bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, inv, ns, t_min, t_best, te);
     if (h0) k0 = te;
-    const bool h1 = (c1 != kEmptyChild) && slab(nd.box[1], o, inv, t_min, t_best, te);
+    const bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, inv, ns, t_min, t_best, te);
     if (h1) k1 = te;
-    const bool h2 = (c2 != kEmptyChild) && slab(nd.box[2], o, inv, t_min, t_best, te);
+    const bool h2 = (c2 != kEmptyChild) && slab_s(nd.box[2], o, inv, ns, t_min, t_best, te);
     if (h2) k2 = te;
-    const bool h3 = (c3 != kEmptyChild) && slab(nd.box[3], o, inv, t_min, t_best, te);
+    const bool h3 = (c3 != kEmptyChild) && slab_s(nd.box[3], o, inv, ns, t_min, t_best, te);
     if (h3) k3 = te;
     visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
     // hit leaf children, in child order

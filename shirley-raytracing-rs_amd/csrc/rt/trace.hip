@@ -67,7 +67,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
   const unsigned long long pix_per_chunk = (unsigned long long)W.n_tiles_rank * kTilePixels;
 
 #ifdef RT_PHASE_TIMING
-  unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0;
+  unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
 #endif
   for (;;) {
 #ifdef RT_PHASE_TIMING
@@ -147,13 +147,19 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
 #ifdef RT_PHASE_TIMING
     const unsigned long long ph1 = clock64();
     ph_regen += ph1 - ph0;
+    const unsigned long long ph_before = ph_lane_steps;
 #endif
     if (active) {
       ++n_seg;
       double t_best = __builtin_inf();
       int face = -1;
+#ifdef RT_PHASE_TIMING
+      int prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits,
+                                          ptests, ph_lane_steps);
+#else
       int prim =
           traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
+#endif
 #ifdef RT_PHASE_TIMING
       const unsigned long long ph2 = clock64();
       ph_trav += ph2 - ph1;
@@ -178,6 +184,13 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
       ph_shade += clock64() - ph2;
 #endif
     }
+#ifdef RT_PHASE_TIMING
+    {
+      unsigned dl = (unsigned)(ph_lane_steps - ph_before);  // this lane's steps (0 when idle)
+      for (int off = 32; off > 0; off >>= 1) dl = max(dl, (unsigned)__shfl_xor((int)dl, off));
+      ph_wave_steps += dl;  // the wave's loop iterations = its slowest lane's steps
+    }
+#endif
     if (visits > (1u << 30)) { n_vis += visits; visits = 0; }
     if (ptests > (1u << 30)) { n_pt += ptests; ptests = 0; }
   }
@@ -190,6 +203,10 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     n_vis += __shfl_down(n_vis, off);
     n_pt += __shfl_down(n_pt, off);
   }
+#ifdef RT_PHASE_TIMING
+  for (int off = 32; off > 0; off >>= 1) ph_lane_steps += __shfl_down(ph_lane_steps, off);
+  if (lane == 0) atomicAdd(&P.counters[blockIdx.x % kCounterSlots].pad[3], ph_lane_steps);
+#endif
   if (lane == 0) {
     DCounters* cs = P.counters + (blockIdx.x % kCounterSlots);
     atomicAdd(&cs->segments, n_seg);
@@ -200,6 +217,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     atomicAdd(&cs->pad[0], ph_regen);
     atomicAdd(&cs->pad[1], ph_trav);
     atomicAdd(&cs->pad[2], ph_shade);
+    atomicAdd(&cs->pad[4], ph_wave_steps);
 #endif
   }
 }
