@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     return ap.parse_args()
 
 
@@ -79,9 +81,15 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # --dist-backend gloo + fewer GPUs than ranks: a rehearsal of the multi-rank path on one box
+    # (ranks share GPUs round-robin); the measured configuration is nccl (RCCL over xGMI)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     scene = rt.SceneBuilder.builtin(args.scene, args.seed).finalize(args.seed)
     cam = rt.scene_camera(args.scene, args.width, args.aspect)
@@ -129,7 +137,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

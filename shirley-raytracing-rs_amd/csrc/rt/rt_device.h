@@ -553,6 +553,91 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_node
   return best;
 }
 
+// One node visit of the 4-wide traversal (the body of traverse4's loop) for the postponed-shading
+// megakernel, where a ray's traversal state lives across other lanes' shading.
+struct Trav4 {
+  v3 inv;
+  double a, t_best;
+  int best, face, node, sp, steps;
+  RaySigns ns;
+};
+
+__device__ __forceinline__ void trav4_begin(Trav4& T, v3 d, double t_max) {
+  T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  T.ns = ray_signs(T.inv);
+  T.a = len2(d);
+  T.t_best = t_max;
+  T.best = -1;
+  T.face = -1;
+  T.node = 0;
+  T.sp = 0;
+  T.steps = 0;
+}
+
+// Returns true when the traversal is complete (T.best / T.t_best / T.face hold the closest hit).
+template <int STRIDE, int MODE>
+__device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4* lds_nodes, const DPrim* lds_prims, v3 o,
+                                           v3 d, double t_min, Trav4& T, int* stk_node, float* stk_t,
+                                           unsigned& visits, unsigned& ptests) {
+  if (++T.steps > S.n_nodes4) return true;  // defect guard (a traversal visits each node at most once)
+  const double kInf = __builtin_inf();
+  const DNode4& nd = fetch_node4<MODE>(S, lds_nodes, T.node);
+  int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
+  double k0 = kInf, k1 = kInf, k2 = kInf, k3 = kInf;
+  double te;
+  const bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, T.inv, T.ns, t_min, T.t_best, te);
+  if (h0) k0 = te;
+  const bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, T.inv, T.ns, t_min, T.t_best, te);
+  if (h1) k1 = te;
+  const bool h2 = (c2 != kEmptyChild) && slab_s(nd.box[2], o, T.inv, T.ns, t_min, T.t_best, te);
+  if (h2) k2 = te;
+  const bool h3 = (c3 != kEmptyChild) && slab_s(nd.box[3], o, T.inv, T.ns, t_min, T.t_best, te);
+  if (h3) k3 = te;
+  visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
+  unsigned lm = (h0 && c0 < 0 ? 1u : 0u) | (h1 && c1 < 0 ? 2u : 0u) | (h2 && c2 < 0 ? 4u : 0u) |
+                (h3 && c3 < 0 ? 8u : 0u);
+#pragma unroll 1
+  while (lm) {
+    const int k = __builtin_ctz(lm);
+    lm &= lm - 1;
+    const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
+    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
+    double t;
+    int f = -1;
+    ++ptests;
+    if (prim_t(pr, o, d, T.a, t_min, T.t_best, t, f)) { T.t_best = t; T.best = leaf; T.face = f; }
+  }
+  if (c0 < 0) k0 = kInf;
+  if (c1 < 0) k1 = kInf;
+  if (c2 < 0) k2 = kInf;
+  if (c3 < 0) k3 = kInf;
+  cas(k0, c0, k1, c1);
+  cas(k2, c2, k3, c3);
+  cas(k0, c0, k2, c2);
+  cas(k1, c1, k3, c3);
+  cas(k1, c1, k2, c2);
+  const double tb = T.t_best;
+  int sp = T.sp;
+  if (k3 < kInf && k3 <= tb) { stk_node[sp * STRIDE] = c3; stk_t[sp * STRIDE] = __double2float_rd(k3); ++sp; }
+  if (k2 < kInf && k2 <= tb) { stk_node[sp * STRIDE] = c2; stk_t[sp * STRIDE] = __double2float_rd(k2); ++sp; }
+  if (k1 < kInf && k1 <= tb) { stk_node[sp * STRIDE] = c1; stk_t[sp * STRIDE] = __double2float_rd(k1); ++sp; }
+  if (k0 < kInf && k0 <= tb) {
+    T.node = c0;
+    T.sp = sp;
+    return false;
+  }
+  while (sp > 0) {
+    --sp;
+    if ((double)stk_t[sp * STRIDE] <= tb) {
+      T.node = stk_node[sp * STRIDE];
+      T.sp = sp;
+      return false;
+    }
+  }
+  T.sp = 0;
+  return true;
+}
+
 template <int MODE>
 __device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4* lds_nodes, DPrim* lds_prims) {
   if (MODE == kNodesGlobal) return;

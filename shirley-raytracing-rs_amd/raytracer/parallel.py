@@ -49,10 +49,13 @@ def gather_tiles(packed, world: int):
     CUDA tensors; gloo for CPU tensors in the tests)."""
     import torch
     import torch.distributed as dist
-    if packed.is_cuda:
+    if packed.is_cuda and dist.get_backend() == "nccl":
         out = torch.empty((world,) + tuple(packed.shape), dtype=packed.dtype, device=packed.device)
         dist.all_gather_into_tensor(out, packed.contiguous())
         return out
-    parts = [torch.empty_like(packed) for _ in range(world)]
-    dist.all_gather(parts, packed.contiguous())
-    return torch.stack(parts)
+    # gloo (CPU tests, single-GPU rehearsals): gather host copies, hand back a tensor on the
+    # input's device
+    host = packed.detach().to("cpu").contiguous()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host)
+    return torch.stack(parts).to(packed.device)
