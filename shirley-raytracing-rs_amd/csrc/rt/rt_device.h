@@ -677,8 +677,11 @@ __device__ __forceinline__ int32_t sat_i32(double x) {
 
 // perlin/mod.rs:87-109 + interp 40-63.  The six permutation entries and then the eight gradient
 // vectors are fetched as independent loads (the corner loop of the reference serialises four
-// dependent loads per corner); the accumulation runs in the reference's (di, dj, dk) order with
-// its exact expressions, so the value is bit-identical.
+// dependent loads per corner).  The accumulation runs in the reference's (di, dj, dk) order with its
+// product order ((wx wy) wz) dot.  Its corner weights `i*uu + (1-i)*(1-uu)` with i in {0.0, 1.0}
+// are exactly `1 - uu` and `uu`: uu = u*u*(3-2u) lies in [0, 1] for u in [0, 1) (it rounds to at
+// most 1.0), so 0*uu and 0*(1-uu) are +0, 1*x is x and x + 0 is x; for a NaN u both forms are NaN.
+// So the value is bit-identical with a third of the reference's arithmetic.
 __device__ __forceinline__ double perlin_noise_inl(const DPerlin* T, v3 p) {
   double xf = floor(p.x), yf = floor(p.y), zf = floor(p.z);
   double u = p.x - xf, v = p.y - yf, w = p.z - zf;
@@ -689,22 +692,20 @@ __device__ __forceinline__ double perlin_noise_inl(const DPerlin* T, v3 p) {
   const int px[2] = {T->perm_x[i & 0xFF], T->perm_x[(i + 1) & 0xFF]};
   const int py[2] = {T->perm_y[j & 0xFF], T->perm_y[(j + 1) & 0xFF]};
   const int pz[2] = {T->perm_z[k & 0xFF], T->perm_z[(k + 1) & 0xFF]};
+  const double wx[2] = {1.0 - uu, uu}, wy[2] = {1.0 - vv, vv}, wz[2] = {1.0 - ww, ww};
+  const double gx[2] = {u, u - 1.0}, gy[2] = {v, v - 1.0}, gz[2] = {w, w - 1.0};  // u - i (u - 0.0 == u)
   double accum = 0.0;
 #pragma unroll
   for (int di = 0; di < 2; ++di) {
-    const double fi = (double)di;
 #pragma unroll
     for (int dj = 0; dj < 2; ++dj) {
-      const double fj = (double)dj;
       const int pxy = px[di] ^ py[dj];
+      const double wxy = wx[di] * wy[dj];
 #pragma unroll
       for (int dk = 0; dk < 2; ++dk) {
-        const double fk = (double)dk;
         const int idx = pxy ^ pz[dk];
-        v3 c = V(T->ranfloat[idx][0], T->ranfloat[idx][1], T->ranfloat[idx][2]);
-        v3 weight = V(u - fi, v - fj, w - fk);
-        accum += (fi * uu + (1.0 - fi) * (1.0 - uu)) * (fj * vv + (1.0 - fj) * (1.0 - vv)) *
-                 (fk * ww + (1.0 - fk) * (1.0 - ww)) * dot(c, weight);
+        const v3 c = V(T->ranfloat[idx][0], T->ranfloat[idx][1], T->ranfloat[idx][2]);
+        accum += (wxy * wz[dk]) * dot(c, V(gx[di], gy[dj], gz[dk]));
       }
     }
   }
