@@ -61,6 +61,7 @@ struct rt_ctx {
   DScene wf_scene{};
   int wf_blocks_per_cu = 0;
   bool has_perlin = false;
+  int n_perlin = 0;
   // per-render scratch
   DevBuf partial, accum, counters, unit_counter;
   DevBuf wf_pool, wf_iters;          // path slots (SoA) + texture queue; per-iteration counters ring
@@ -457,6 +458,7 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
   P.work = kp.work;
   wf_carve(c->wf_pool.p, n, P);
   P.n_slots = (uint32_t)n;
+  P.n_perlin = c->n_perlin;
   P.partial = kp.partial;
   P.unit_counter = kp.unit_counter;
   P.counters = kp.counters;
@@ -469,6 +471,7 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
   const int gt = wf_grid_threads();
   const int grid = (int)((n + gt - 1) / gt);
   const bool texture_pass = c->has_perlin;  // deferred entries exist only for Perlin leaves
+  const int tex_grid = std::min(grid, 4 * c->cu_count);  // strided over slot groups, tables staged once per block
   const int ext_blocks = std::max(1, c->cu_count * std::max(1, c->wf_blocks_per_cu));
 
   // timing: an event before and after each launch of a round, elapsed times summed per kernel
@@ -500,7 +503,7 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
       if ((st = lap_mark(1))) return st;
       HIP_TRY(c, wf_launch_shade(P, grid, s));
       if ((st = lap_mark(2))) return st;
-      if (texture_pass) HIP_TRY(c, wf_launch_texture(P, grid, s));
+      if (texture_pass) HIP_TRY(c, wf_launch_texture(P, tex_grid, s));
       if ((st = lap_mark(3))) return st;
     }
     HIP_TRY(c, hipMemcpyAsync(&c->wf_host[batch & 1], P.retired, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -805,6 +808,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   HIP_TRY(c, wf_prepare(W, &wbpc));
   if (wbpc < 1) return fail(c, RT_E_UNSUPPORTED, "wavefront extend kernel does not fit on a CU");
   c->wf_scene = W;
+  c->n_perlin = d->n_perlin;
   c->has_perlin = false;
   for (int i = 0; i < d->n_textures; ++i) c->has_perlin |= d->textures[i].kind == RT_TEX_PERLIN;
   c->wf_blocks_per_cu = wbpc;

@@ -181,6 +181,7 @@ struct WfParams {
   WfTexQ tq;
   uint32_t n_slots;     // multiple of 64: slot group g = slots [64 g, 64 g + 64) = one wave of wf_shade
   uint32_t first;       // wf_shade's first round: group g's unit window is [64 g, 64 g + 64)
+  int32_t n_perlin;     // Perlin tables of the scene (wf_texture copies up to 2 into LDS)
   double* partial;
   unsigned long long* unit_counter;  // dynamic units are n_slots + the counter (64 per fetch)
   unsigned long long* win;           // per group: [next, end) of its unit window

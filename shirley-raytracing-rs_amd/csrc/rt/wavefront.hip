@@ -411,36 +411,52 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
 }
 
 // ------------------------------------------------------------------------------------------
-// wf_texture: deferred Perlin texture values; wave g evaluates group g's compacted entries
+// wf_texture: deferred Perlin texture values.  Blocks stride over the slot groups (wave w of a block
+// takes group base + w); each block first copies the scene's Perlin tables (9 KB each) into LDS when
+// they fit, so the ~210 table gathers of a marble evaluation are LDS reads.
 // ------------------------------------------------------------------------------------------
+constexpr int kTexLdsTables = 2;
+
+template <bool LDS_TABLES>
 __global__ __launch_bounds__(kGridThreads) void wf_texture(WfParams P) {
+  __shared__ DPerlin tabs[LDS_TABLES ? kTexLdsTables : 1];
   const DScene& S = P.scene;
   const WfState& st = P.st;
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t g = i / kWave;
-  if (i >= P.n_slots) return;
-  const uint32_t n = P.tq.count[g];
-  if ((uint32_t)__lane_id() >= n) return;
-  const int slot = P.tq.slot[i];
-  const DTex& t = S.texs[P.tq.tex[i]];
-  const v3 p = V(P.tq.px[i], P.tq.py[i], P.tq.pz[i]);
-  const double nz = marble_inl(S.perlin + t.table, t.scale, p);  // perlin/mod.rs:162-183
-  v3 a = V(nz, nz, nz);
-  v3 att = V(st.ax[slot], st.ay[slot], st.az[slot]);
-  const int kind = P.tq.kind[i];
-  if (kind == kDeferLambertian) {
-    att = hmul(att, a);
-  } else if (kind == kDeferFairy) {  // emitted (lighting.rs:59-66) before the scatter attenuation
-    v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
-    em = em + hmul(att, scale(a, P.tq.scale[i]));
-    st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
-    att = hmul(att, unit(a));
-  } else {  // DiffuseLight
-    v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
-    em = em + hmul(att, a);
-    st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
+  if (LDS_TABLES) {
+    const int4* src = reinterpret_cast<const int4*>(S.perlin);
+    int4* dst = reinterpret_cast<int4*>(tabs);
+    const int n16 = P.n_perlin * (int)(sizeof(DPerlin) / 16);
+    for (int k = threadIdx.x; k < n16; k += blockDim.x) dst[k] = src[k];
+    __syncthreads();
   }
-  st.ax[slot] = att.x; st.ay[slot] = att.y; st.az[slot] = att.z;
+  const DPerlin* perlin = LDS_TABLES ? tabs : S.perlin;
+  const uint32_t n_groups = P.n_slots / kWave;
+  const uint32_t waves = blockDim.x / kWave;
+  for (uint32_t g = blockIdx.x * waves + threadIdx.x / kWave; g < n_groups; g += gridDim.x * waves) {
+    const uint32_t n = P.tq.count[g];
+    if ((uint32_t)__lane_id() >= n) continue;
+    const uint32_t i = g * kWave + __lane_id();
+    const int slot = P.tq.slot[i];
+    const DTex& t = S.texs[P.tq.tex[i]];
+    const v3 p = V(P.tq.px[i], P.tq.py[i], P.tq.pz[i]);
+    const double nz = marble_inl(perlin + t.table, t.scale, p);  // perlin/mod.rs:162-183
+    v3 a = V(nz, nz, nz);
+    v3 att = V(st.ax[slot], st.ay[slot], st.az[slot]);
+    const int kind = P.tq.kind[i];
+    if (kind == kDeferLambertian) {
+      att = hmul(att, a);
+    } else if (kind == kDeferFairy) {  // emitted (lighting.rs:59-66) before the scatter attenuation
+      v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
+      em = em + hmul(att, scale(a, P.tq.scale[i]));
+      st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
+      att = hmul(att, unit(a));
+    } else {  // DiffuseLight
+      v3 em = V(st.ex[slot], st.ey[slot], st.ez[slot]);
+      em = em + hmul(att, a);
+      st.ex[slot] = em.x; st.ey[slot] = em.y; st.ez[slot] = em.z;
+    }
+    st.ax[slot] = att.x; st.ay[slot] = att.y; st.az[slot] = att.z;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -498,7 +514,10 @@ hipError_t wf_launch_shade(const WfParams& P, int grid_blocks, hipStream_t s) {
 }
 
 hipError_t wf_launch_texture(const WfParams& P, int grid_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(wf_texture, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+  if (P.n_perlin <= kTexLdsTables)
+    hipLaunchKernelGGL(wf_texture<true>, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+  else
+    hipLaunchKernelGGL(wf_texture<false>, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
   return hipGetLastError();
 }
 
