@@ -32,6 +32,8 @@ size_t wf_extend_lds(int n_lds_nodes, int stack_depth);
 int wf_extend_threads();
 int wf_grid_threads();
 hipError_t wf_prepare(const DScene& S, int* extend_blocks_per_cu);
+hipError_t wf_prepare4(const DScene& S, int* extend_blocks_per_cu);
+hipError_t wf_launch_extend4(const WfParams& P, int extend_blocks, hipStream_t s);
 hipError_t wf_start(const WfParams& P, int grid_blocks, hipStream_t s);
 hipError_t wf_launch_extend(const WfParams& P, int extend_blocks, hipStream_t s);
 hipError_t wf_launch_shade(const WfParams& P, int grid_blocks, hipStream_t s);
@@ -60,6 +62,8 @@ struct rt_ctx {
   // wavefront engine: the scene with its LDS node count sized for the extend block
   DScene wf_scene{};
   int wf_blocks_per_cu = 0;
+  bool wf_wide = false;      // wavefront extend runs the 4-wide scene-in-LDS kernel (wf_extend4)
+  int wf4_blocks_per_cu = 0;
   bool has_perlin = false;
   int n_perlin = 0;
   // per-render scratch
@@ -266,7 +270,7 @@ double half_area(const Box& b) {
 // it has fewer than four, replaces its largest-area internal child by that child's two children
 // (order kept).  Boxes stay the reference's exact boxes.  `stack_bound` = the worst-case traversal
 // stack: the sum over a root path of (internal children - 1) per node (at most that many pushes).
-void flatten4(const BuiltTree& t, std::vector<DNode4>& out, int32_t& stack_bound) {
+void flatten4(const BuiltTree& t, const rt_scene_desc* d, std::vector<DNode4>& out, int32_t& stack_bound) {
   out.clear();
   DNode4 top{};
   for (int k = 0; k < 4; ++k) top.child[k] = kEmptyChild;
@@ -286,7 +290,8 @@ void flatten4(const BuiltTree& t, std::vector<DNode4>& out, int32_t& stack_bound
     const BuildNode& bn = t.nodes[it.built];
     box_to_node(bn.box, out[it.parent].box[it.slot]);
     if (bn.leaf >= 0) {
-      out[it.parent].child[it.slot] = ~bn.leaf;
+      const bool sphere = d->objects[bn.leaf].geometry == RT_GEOM_SPHERE;
+      out[it.parent].child[it.slot] = ~(bn.leaf | (sphere ? 0 : kLeafGeneric));
       continue;
     }
     const int32_t idx = (int32_t)out.size();
@@ -459,6 +464,8 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
   wf_carve(c->wf_pool.p, n, P);
   P.n_slots = (uint32_t)n;
   P.n_perlin = c->n_perlin;
+  P.ext_window = 256;
+  if (const char* e = getenv("SHIRLEY_WF_WINDOW")) P.ext_window = (uint32_t)std::max(1, atoi(e) / 64) * 64;
   P.partial = kp.partial;
   P.unit_counter = kp.unit_counter;
   P.counters = kp.counters;
@@ -499,7 +506,10 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
   for (;;) {
     for (int k = 0; k < kWfBatch; ++k, ++iter) {
       if ((st = lap_mark(0))) return st;
-      HIP_TRY(c, wf_launch_extend(P, ext_blocks, s));
+      if (c->wf_wide)
+        HIP_TRY(c, wf_launch_extend4(P, c->cu_count * c->wf4_blocks_per_cu, s));
+      else
+        HIP_TRY(c, wf_launch_extend(P, ext_blocks, s));
       if ((st = lap_mark(1))) return st;
       HIP_TRY(c, wf_launch_shade(P, grid, s));
       if ((st = lap_mark(2))) return st;
@@ -677,6 +687,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const int32_t placement = builder & placement_mask;
   builder &= ~placement_mask;
   if (builder != RT_BVH_REFERENCE && builder != RT_BVH_SAH) return fail(c, RT_E_INVALID, "bad bvh builder %d", builder);
+  if (d->n_objects >= kLeafGeneric) return fail(c, RT_E_UNSUPPORTED, "too many objects (%d)", d->n_objects);
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->have_scene = false;
@@ -686,7 +697,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   flatten(tree, nodes);
   std::vector<DNode4> nodes4;
   int32_t stack4 = 1;
-  flatten4(tree, nodes4, stack4);
+  flatten4(tree, d, nodes4, stack4);
   std::vector<DPrim> prims(std::max(1, d->n_objects));
   for (int i = 0; i < d->n_objects; ++i) {
     const rt_object& o = d->objects[i];
@@ -808,6 +819,16 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   HIP_TRY(c, wf_prepare(W, &wbpc));
   if (wbpc < 1) return fail(c, RT_E_UNSUPPORTED, "wavefront extend kernel does not fit on a CU");
   c->wf_scene = W;
+  c->wf_wide = false;
+  if (c->mk_threads == kTraceThreadsWide && S.n_lds_prims > 0 && !getenv("SHIRLEY_WF_EXTEND2")) {
+    int b4 = 0;
+    HIP_TRY(c, wf_prepare4(S, &b4));
+    if (b4 >= 1) {
+      c->wf_wide = true;
+      c->wf4_blocks_per_cu = b4;
+      c->wf_scene = S;  // wf_extend4 reads the megakernel's LDS layout
+    }
+  }
   c->n_perlin = d->n_perlin;
   c->has_perlin = false;
   for (int i = 0; i < d->n_textures; ++i) c->has_perlin |= d->textures[i].kind == RT_TEX_PERLIN;

@@ -456,6 +456,49 @@ __device__ __forceinline__ const DNode4& fetch_node4(const DScene& S, const DNod
   return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : S.nodes4[idx];
 }
 
+// The hit leaf children of a 4-wide node against the running closest (bbox_tree.rs:60-71): sphere
+// leaves first in their own loop (sphere.rs:28-46 only), then rect / box leaves with the generic test,
+// each in child order.  A wave thus runs the rect / box code only when one of its lanes holds such a
+// leaf, and never once per sphere leaf.
+template <int MODE>
+__device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, double a,
+                                            double t_min, bool h0, bool h1, bool h2, bool h3, int c0, int c1,
+                                            int c2, int c3, double& t_best, int& best, int& face_best,
+                                            unsigned& ptests) {
+  auto kind = [](bool h, int c, unsigned bit, unsigned& sph, unsigned& gen) {
+    if (h && c < 0) {
+      if ((~c) & kLeafGeneric) gen |= bit;
+      else sph |= bit;
+    }
+  };
+  unsigned sph = 0, gen = 0;
+  kind(h0, c0, 1u, sph, gen);
+  kind(h1, c1, 2u, sph, gen);
+  kind(h2, c2, 4u, sph, gen);
+  kind(h3, c3, 8u, sph, gen);
+#pragma unroll 1
+  while (sph) {
+    const int k = __builtin_ctz(sph);
+    sph &= sph - 1;
+    const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
+    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
+    double t;
+    ++ptests;
+    if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; }
+  }
+#pragma unroll 1
+  while (gen) {
+    const int k = __builtin_ctz(gen);
+    gen &= gen - 1;
+    const int leaf = (~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3)) & (kLeafGeneric - 1);
+    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
+    double t;
+    int f = -1;
+    ++ptests;
+    if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; }
+  }
+}
+
 // compare-exchange of (key, node) pairs: ascending key
 __device__ __forceinline__ void cas(double& ka, int& na, double& kb, int& nb) {
   const bool sw = kb < ka;
@@ -507,20 +550,8 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_node
     const bool h3 = (c3 != kEmptyChild) && slab_s(nd.box[3], o, inv, ns, t_min, t_best, te);
     if (h3) k3 = te;
     visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
-    // hit leaf children, in child order
-    unsigned lm = (h0 && c0 < 0 ? 1u : 0u) | (h1 && c1 < 0 ? 2u : 0u) | (h2 && c2 < 0 ? 4u : 0u) |
-                  (h3 && c3 < 0 ? 8u : 0u);
-#pragma unroll 1
-    while (lm) {
-      const int k = __builtin_ctz(lm);
-      lm &= lm - 1;
-      const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
-      const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-      double t;
-      int f = -1;
-      ++ptests;
-      if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; }
-    }
+    // hit leaf children: spheres in a tight loop, then rects / boxes
+    leaf_tests4<MODE>(S, lds_prims, o, d, a, t_min, h0, h1, h2, h3, c0, c1, c2, c3, t_best, best, face_best, ptests);
     // internal children nearest-first: leaves and misses sort last (key inf)
     if (c0 < 0) k0 = kInf;
     if (c1 < 0) k1 = kInf;
@@ -594,19 +625,7 @@ __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4* lds_no
   const bool h3 = (c3 != kEmptyChild) && slab_s(nd.box[3], o, T.inv, T.ns, t_min, T.t_best, te);
   if (h3) k3 = te;
   visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
-  unsigned lm = (h0 && c0 < 0 ? 1u : 0u) | (h1 && c1 < 0 ? 2u : 0u) | (h2 && c2 < 0 ? 4u : 0u) |
-                (h3 && c3 < 0 ? 8u : 0u);
-#pragma unroll 1
-  while (lm) {
-    const int k = __builtin_ctz(lm);
-    lm &= lm - 1;
-    const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
-    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-    double t;
-    int f = -1;
-    ++ptests;
-    if (prim_t(pr, o, d, T.a, t_min, T.t_best, t, f)) { T.t_best = t; T.best = leaf; T.face = f; }
-  }
+  leaf_tests4<MODE>(S, lds_prims, o, d, T.a, t_min, h0, h1, h2, h3, c0, c1, c2, c3, T.t_best, T.best, T.face, ptests);
   if (c0 < 0) k0 = kInf;
   if (c1 < 0) k1 = kInf;
   if (c2 < 0) k2 = kInf;

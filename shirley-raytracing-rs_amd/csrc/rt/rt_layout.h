@@ -32,7 +32,10 @@ struct alignas(16) DNode {
 static_assert(sizeof(DNode) == 112, "DNode layout");
 
 // 4-wide node of the collapsed tree used by the megakernel (fewer dependent node fetches per ray);
-// same exact f64 child boxes and child encoding as DNode.
+// same exact f64 child boxes and child encoding as DNode, except that a leaf child that is not a
+// sphere carries kLeafGeneric in its primitive index (~(prim | kLeafGeneric)), so traversal can test
+// sphere leaves in a tight loop and rects / boxes in a second one without loading the primitive first.
+constexpr int32_t kLeafGeneric = 1 << 29;
 struct alignas(16) DNode4 {
   double box[4][6];
   int32_t child[4];
@@ -182,6 +185,7 @@ struct WfParams {
   uint32_t n_slots;     // multiple of 64: slot group g = slots [64 g, 64 g + 64) = one wave of wf_shade
   uint32_t first;       // wf_shade's first round: group g's unit window is [64 g, 64 g + 64)
   int32_t n_perlin;     // Perlin tables of the scene (wf_texture copies up to 2 into LDS)
+  uint32_t ext_window;  // wf_extend4: slots a wave claims per cursor atomic (multiple of 64)
   double* partial;
   unsigned long long* unit_counter;  // dynamic units are n_slots + the counter (64 per fetch)
   unsigned long long* win;           // per group: [next, end) of its unit window

@@ -37,14 +37,14 @@ __device__ __forceinline__ unsigned long long wf_lanemask_lt() {
 // ------------------------------------------------------------------------------------------
 // Next 64-slot window for a wave: queue q first, then the following queues once q is drained.
 // Returns the window's first slot, or ~0 when every queue is drained.  Lane 0 does the work.
-__device__ __forceinline__ unsigned long long next_window(WfIter* it, int& q, uint32_t qlen) {
+__device__ __forceinline__ unsigned long long next_window(WfIter* it, int& q, uint32_t qlen, uint32_t win) {
   unsigned long long base = ~0ull;
   int qq = q;
   if (__lane_id() == 0) {
     for (int tries = 0; tries < kWfQueues; ++tries) {
       unsigned long long* cur = &it->fetch[qq][0];
       if (__hip_atomic_load(cur, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < qlen) {
-        const unsigned long long nb = atomicAdd(cur, (unsigned long long)kWave);
+        const unsigned long long nb = atomicAdd(cur, (unsigned long long)win);
         if (nb < qlen) {
           base = (unsigned long long)qq * qlen + nb;
           break;
@@ -84,7 +84,7 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
     const unsigned long long mask = __ballot(need);
     if (mask != 0ull && !exhausted) {
       if (w_next == w_end) {
-        const unsigned long long nb = next_window(P.it, q, qlen);
+        const unsigned long long nb = next_window(P.it, q, qlen, kWave);
         if (nb == ~0ull) {
           exhausted = true;
         } else {
@@ -129,6 +129,103 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
     atomicAdd(&cs->node_visits, v);
     atomicAdd(&cs->prim_tests, pt);
     atomicAdd(&cs->segments, r);  // ray_color loop iterations that traced a ray (render.rs:31)
+  }
+}
+
+// wf_extend4: the same closest-hit pass for scenes whose 4-wide tree and primitives fit in LDS next
+// to the stacks (the megakernel's wide configuration).  Traversal then issues no global loads, and
+// each lane prefetches its NEXT ray (state, origin, direction) while it traverses the current one:
+// the refill latency (path state of 2 M slots lives in HBM) is hidden behind the traversal steps.
+template <int THREADS>
+__global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
+  extern __shared__ unsigned char lds_raw[];
+  const int tid = threadIdx.x;
+  DNode4* lds_nodes = reinterpret_cast<DNode4*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4));
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4) +
+                            (size_t)P.scene.n_lds_prims * sizeof(DPrim);
+  int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
+  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
+  stage_nodes4<kSceneLds>(P.scene, lds_nodes, lds_prims);
+  const DScene& S = P.scene;
+  const WfState& st = P.st;
+  const int lane = __lane_id();
+  const uint32_t win = P.ext_window;  // slots per cursor claim (a multiple of 64)
+  const uint32_t qlen = (P.n_slots / kWfQueues + win) / win * win;
+  int q = (int)((blockIdx.x * (THREADS / kWave) + tid / kWave) % kWfQueues);
+
+  unsigned long long w_next = 0, w_end = 0;
+  bool exhausted = false, active = false, has_next = false;
+  int slot = 0, nslot = 0;
+  uint8_t nstate = 0;
+  v3 o = V(0, 0, 0), d = V(0, 0, 0), no = V(0, 0, 0), nd = V(0, 0, 0);
+  Trav4 T;
+  trav4_begin(T, V(1.0, 1.0, 1.0), 0.0);
+  unsigned visits = 0, ptests = 0, rays = 0;
+  for (;;) {
+    // A. a lane without a ray takes its prefetched one (if that slot holds a ray)
+    if (!active && has_next) {
+      has_next = false;
+      if (nstate == kSlotAlive) {
+        slot = nslot;
+        o = no;
+        d = nd;
+        trav4_begin(T, d, __builtin_inf());
+        active = true;
+        ++rays;
+      }
+    }
+    // B. lanes without a prefetched ray claim the next slot of the wave's window and issue its loads
+    const bool need = !has_next;
+    const unsigned long long mask = __ballot(need);
+    if (mask != 0ull && !exhausted) {
+      if (w_next == w_end) {
+        const unsigned long long nb = next_window(P.it, q, qlen, win);
+        if (nb == ~0ull) {
+          exhausted = true;
+        } else {
+          w_next = nb;
+          w_end = nb + win;
+        }
+      }
+      if (!exhausted) {
+        const unsigned long long avail = w_end - w_next;
+        const unsigned long long rank = __popcll(mask & wf_lanemask_lt());
+        const unsigned long long idx = w_next + rank;
+        w_next += min((unsigned long long)__popcll(mask), avail);
+        if (need && rank < avail && idx < P.n_slots) {
+          nslot = (int)idx;
+          nstate = st.state[nslot];
+          no = V(st.ox[nslot], st.oy[nslot], st.oz[nslot]);
+          nd = V(st.dx[nslot], st.dy[nslot], st.dz[nslot]);
+          has_next = true;
+        }
+      }
+    }
+    if (!__any(active || has_next)) {
+      if (exhausted) break;
+      continue;
+    }
+    // C. one node visit for every lane holding a ray
+    if (active && trav4_step<THREADS, kSceneLds>(S, lds_nodes, lds_prims, o, d, 0.001, T, stk_node, stk_t, visits,
+                                                 ptests)) {
+      st.ht[slot] = T.t_best;
+      st.hprim[slot] = T.best;
+      st.hface[slot] = T.face;
+      active = false;
+    }
+  }
+  unsigned long long v = visits, pt = ptests, r = rays;
+  for (int off = 32; off > 0; off >>= 1) {
+    v += __shfl_down(v, off);
+    pt += __shfl_down(pt, off);
+    r += __shfl_down(r, off);
+  }
+  if (lane == 0) {
+    DCounters* cs = P.counters + ((blockIdx.x * (THREADS / kWave) + tid / kWave) % kCounterSlots);
+    atomicAdd(&cs->node_visits, v);
+    atomicAdd(&cs->prim_tests, pt);
+    atomicAdd(&cs->segments, r);
   }
 }
 
@@ -470,6 +567,27 @@ int wf_extend_threads() { return kExtendThreads; }
 
 static int wf_mode(const DScene& S) {
   return S.n_lds_nodes >= S.n_nodes ? kNodesLds : (S.n_lds_nodes == 0 ? kNodesGlobal : kNodesMixed);
+}
+
+size_t wf_extend4_lds(const DScene& S) {
+  return (size_t)S.n_lds_nodes4 * sizeof(DNode4) + (size_t)S.n_lds_prims * sizeof(DPrim) +
+         (size_t)S.stack_depth4 * kTraceThreadsWide * 8;
+}
+
+// The 4-wide, scene-in-LDS extend kernel for scenes where the megakernel runs wide (`S` = that scene).
+hipError_t wf_prepare4(const DScene& S, int* extend_blocks_per_cu) {
+  const int lds = (int)wf_extend4_lds(S);
+  hipError_t e = hipFuncSetAttribute((const void*)wf_extend4<kTraceThreadsWide>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend4<kTraceThreadsWide>,
+                                                       kTraceThreadsWide, lds);
+}
+
+hipError_t wf_launch_extend4(const WfParams& P, int extend_blocks, hipStream_t s) {
+  hipLaunchKernelGGL(wf_extend4<kTraceThreadsWide>, dim3(extend_blocks), dim3(kTraceThreadsWide),
+                     wf_extend4_lds(P.scene), s, P);
+  return hipGetLastError();
 }
 
 hipError_t wf_prepare(const DScene& S, int* extend_blocks_per_cu) {

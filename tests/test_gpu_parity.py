@@ -83,6 +83,21 @@ def test_wavefront_small_slot_pool(gpu, slots, monkeypatch):
         assert (ca.samples, ca.segments) == (cb.samples, cb.segments)
 
 
+def test_wavefront_extend_kernels_agree(gpu, monkeypatch):
+    """wf_extend4 (4-wide tree + primitives in LDS, prefetched rays) and wf_extend (2-wide tree via
+    L1/L2) give the same frame; the 2-wide kernel is the fallback for scenes too big for LDS."""
+    spp = 4
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    cam = rt.default_camera(64, "std16x9")
+    s = rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp, engine="wavefront")  # in-order sums
+    a = gpu.upload(scene, "sah").render(cam, s)
+    monkeypatch.setenv("SHIRLEY_WF_EXTEND2", "1")
+    b = gpu.upload(scene, "sah").render(cam, s)
+    assert np.array_equal(a, b)
+    ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED))
+    check_parity(a, ora, spp)
+
+
 def test_wavefront_timing_counters(gpu):
     """Per-launch event timing; the perlin scene has deferred texture work (a scene without Perlin
     textures skips the wf_texture launch)."""
