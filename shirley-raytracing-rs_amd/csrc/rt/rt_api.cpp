@@ -270,10 +270,63 @@ double half_area(const Box& b) {
 // it has fewer than four, replaces its largest-area internal child by that child's two children
 // (order kept).  Boxes stay the reference's exact boxes.  `stack_bound` = the worst-case traversal
 // stack: the sum over a root path of (internal children - 1) per node (at most that many pushes).
-void flatten4(const BuiltTree& t, const rt_scene_desc* d, std::vector<DNode4>& out, int32_t& stack_bound) {
+// f32 bounds rounded outward (f32 cast rounds to nearest; step once more if it landed inside).
+float round_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+float round_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+// Node-box inflation and the ray-origin range it covers.  The f32 node test computes
+// t = fma(plane, 1/d, -o*(1/d)) from o and 1/d rounded to f32: in space units its error is at most
+// ~2^-22 (|o| + |plane|); inflating every stored box by delta = 2^-20 (L + B) (B = largest finite
+// |plane|) and rounding outward keeps the test a superset of the exact one for every ray with
+// max|o| <= L, with a 4x margin.
+struct Inflation {
+  double delta;
+  float origin_limit;
+};
+Inflation inflation_for(const BuiltTree& t) {
+  double B = 0.0;
+  for (const BuildNode& n : t.nodes)
+    for (int k = 0; k < 3; ++k) {
+      if (std::isfinite(n.box.mn[k])) B = std::max(B, std::fabs(n.box.mn[k]));
+      if (std::isfinite(n.box.mx[k])) B = std::max(B, std::fabs(n.box.mx[k]));
+    }
+  const double L = std::max(16.0, 4.0 * B);
+  return Inflation{std::ldexp(L + B, -20), (float)L};
+}
+
+// child slot of a 4-wide node: an empty slot never passes (lo = +inf > hi = -inf); a box with a
+// NaN plane always passes (its leaf is tested exactly anyway)
+void set_child_box(DNode4F& n, int slot, const Box* b, double delta) {
+  for (int a = 0; a < 3; ++a) {
+    if (!b) {
+      n.lo[a][slot] = INFINITY;
+      n.hi[a][slot] = -INFINITY;
+    } else if (std::isnan(b->mn[a]) || std::isnan(b->mx[a])) {
+      n.lo[a][slot] = -INFINITY;
+      n.hi[a][slot] = INFINITY;
+    } else {
+      n.lo[a][slot] = round_down(b->mn[a] - delta);
+      n.hi[a][slot] = round_up(b->mx[a] + delta);
+    }
+  }
+}
+
+void flatten4(const BuiltTree& t, const rt_scene_desc* d, double delta, std::vector<DNode4F>& out,
+              int32_t& stack_bound) {
   out.clear();
-  DNode4 top{};
-  for (int k = 0; k < 4; ++k) top.child[k] = kEmptyChild;
+  DNode4F top{};
+  for (int k = 0; k < 4; ++k) {
+    top.child[k] = kEmptyChild;
+    set_child_box(top, k, nullptr, delta);
+  }
   out.push_back(top);
   stack_bound = 1;
   if (t.root < 0) return;
@@ -288,7 +341,7 @@ void flatten4(const BuiltTree& t, const rt_scene_desc* d, std::vector<DNode4>& o
   for (size_t head = 0; head < q.size(); ++head) {
     const Item it = q[head];
     const BuildNode& bn = t.nodes[it.built];
-    box_to_node(bn.box, out[it.parent].box[it.slot]);
+    set_child_box(out[it.parent], it.slot, &bn.box, delta);
     if (bn.leaf >= 0) {
       const bool sphere = d->objects[bn.leaf].geometry == RT_GEOM_SPHERE;
       out[it.parent].child[it.slot] = ~(bn.leaf | (sphere ? 0 : kLeafGeneric));
@@ -296,8 +349,11 @@ void flatten4(const BuiltTree& t, const rt_scene_desc* d, std::vector<DNode4>& o
     }
     const int32_t idx = (int32_t)out.size();
     out[it.parent].child[it.slot] = idx;
-    DNode4 nd{};
-    for (int k = 0; k < 4; ++k) nd.child[k] = kEmptyChild;
+    DNode4F nd{};
+    for (int k = 0; k < 4; ++k) {
+      nd.child[k] = kEmptyChild;
+      set_child_box(nd, k, nullptr, delta);
+    }
     out.push_back(nd);
     std::vector<int32_t> ch{bn.lhs, bn.rhs};
     while (ch.size() < 4) {
@@ -695,9 +751,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   BuiltTree tree = build_tree(d, builder);
   std::vector<DNode> nodes;
   flatten(tree, nodes);
-  std::vector<DNode4> nodes4;
+  std::vector<DNode4F> nodes4;
   int32_t stack4 = 1;
-  flatten4(tree, d, nodes4, stack4);
+  const Inflation infl = inflation_for(tree);
+  flatten4(tree, d, infl.delta, nodes4, stack4);
   std::vector<DPrim> prims(std::max(1, d->n_objects));
   for (int i = 0; i < d->n_objects; ++i) {
     const rt_object& o = d->objects[i];
@@ -752,7 +809,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   if (texels.empty()) texels.resize(16);
 
   if ((st = upload(c, c->nodes, nodes.data(), nodes.size() * sizeof(DNode)))) return st;
-  if ((st = upload(c, c->nodes4, nodes4.data(), nodes4.size() * sizeof(DNode4)))) return st;
+  if ((st = upload(c, c->nodes4, nodes4.data(), nodes4.size() * sizeof(DNode4F)))) return st;
   if ((st = upload(c, c->prims, prims.data(), prims.size() * sizeof(DPrim)))) return st;
   if ((st = upload(c, c->mats, mats.data(), mats.size() * sizeof(DMat)))) return st;
   if ((st = upload(c, c->texs, texs.data(), texs.size() * sizeof(DTex)))) return st;
@@ -762,9 +819,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
 
   DScene& S = c->scene;
   S.nodes = static_cast<const DNode*>(c->nodes.p);
-  S.nodes4 = static_cast<const DNode4*>(c->nodes4.p);
+  S.nodes4 = static_cast<const DNode4F*>(c->nodes4.p);
   S.n_nodes4 = (int32_t)nodes4.size();
   S.stack_depth4 = stack4;
+  S.origin_limit = infl.origin_limit;
   S.prims = static_cast<const DPrim*>(c->prims.p);
   S.mats = static_cast<const DMat*>(c->mats.p);
   S.texs = static_cast<const DTex*>(c->texs.p);
@@ -792,13 +850,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
   const long long stack4_bytes = (long long)S.stack_depth4 * kTraceThreads * 8;
   const long long wide_bytes =
-      (long long)S.stack_depth4 * kTraceThreadsWide * 8 + (long long)nodes4.size() * sizeof(DNode4);
+      (long long)S.stack_depth4 * kTraceThreadsWide * 8 + (long long)nodes4.size() * sizeof(DNode4F);
   if (stack_bytes > kLdsBytes || stack4_bytes > kLdsBytes)
     return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
   const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS);
   c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
   S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
-  S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4), nodes4.size());
+  S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4F), nodes4.size());
   // primitives too, when they fit beside the wide block's tree and stacks (leaf tests from LDS)
   const bool prims_lds = wide && wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) <= kLdsBytes &&
                          !getenv("SHIRLEY_NO_LDS_PRIMS");

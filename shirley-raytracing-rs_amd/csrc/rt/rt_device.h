@@ -444,45 +444,114 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
   return best;
 }
 
-// ---- 4-wide traversal (megakernel) ----
+// ---- 4-wide traversal (megakernel, wf_extend4) ----
 #ifdef RT_PHASE_TIMING
 // per-lane step counter of the instrumented build (a register of the calling kernel)
 #define g_trav_lane_steps trav_lane_steps_ref
 #endif
 template <int MODE>
-__device__ __forceinline__ const DNode4& fetch_node4(const DScene& S, const DNode4* lds_nodes, int idx) {
+__device__ __forceinline__ const DNode4F& fetch_node4(const DScene& S, const DNode4F* lds_nodes, int idx) {
   if (MODE == kNodesLds || MODE == kSceneLds) return lds_nodes[idx];
   if (MODE == kNodesGlobal) return S.nodes4[idx];
   return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : S.nodes4[idx];
 }
 
-// The hit leaf children of a 4-wide node against the running closest (bbox_tree.rs:60-71): sphere
-// leaves first in their own loop (sphere.rs:28-46 only), then rect / box leaves with the generic test,
-// each in child order.  A wave thus runs the rect / box code only when one of its lanes holds such a
-// leaf, and never once per sphere leaf.
+// Ray in the form the f32 node test uses: o and 1/d rounded to f32, and o * (1/d) for the FMA.
+struct RayF {
+  float ox, oy, oz, ix, iy, iz, oix, oiy, oiz;
+  bool fast;  // max|o| <= origin_limit: the f32 test's error bound holds
+};
+__device__ __forceinline__ RayF ray_f(const DScene& S, v3 o, v3 inv) {
+  RayF r;
+  r.ox = (float)o.x;
+  r.oy = (float)o.y;
+  r.oz = (float)o.z;
+  r.ix = (float)inv.x;
+  r.iy = (float)inv.y;
+  r.iz = (float)inv.z;
+  r.oix = r.ox * r.ix;
+  r.oiy = r.oy * r.iy;
+  r.oiz = r.oz * r.iz;
+  r.fast = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) <= (double)S.origin_limit;
+  return r;
+}
+
+// Conservative test of child k of a 4-wide node: entry t (lower bound) or +inf when missed.
+// min/max slab form (a NaN from 0 * inf leaves the bound; inverted boxes pass — both only widen).
+__device__ __forceinline__ float node4_child(const DNode4F& nd, int k, const RayF& r, v3 o, v3 inv, float tminf,
+                                             float tmaxf, double t_min, double t_max) {
+  if (r.fast) {
+    const float x0 = fmaf(nd.lo[0][k], r.ix, -r.oix), x1 = fmaf(nd.hi[0][k], r.ix, -r.oix);
+    const float y0 = fmaf(nd.lo[1][k], r.iy, -r.oiy), y1 = fmaf(nd.hi[1][k], r.iy, -r.oiy);
+    const float z0 = fmaf(nd.lo[2][k], r.iz, -r.oiz), z1 = fmaf(nd.hi[2][k], r.iz, -r.oiz);
+    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
+    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
+    return tn <= tf ? tn : __builtin_inff();
+  }
+  // far origins: the same inflated box in f64 (exact arithmetic on a superset box)
+  double tn = t_min, tf = t_max;
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    const double iv = comp(inv, a), oa = comp(o, a);
+    const double t0 = ((double)nd.lo[a][k] - oa) * iv, t1 = ((double)nd.hi[a][k] - oa) * iv;
+    tn = fmax(tn, fmin(t0, t1));
+    tf = fmin(tf, fmax(t0, t1));
+  }
+  return tn <= tf ? __double2float_rd(tn) : __builtin_inff();
+}
+
+// The reference's bounding_box() of a leaf object, exactly: sphere c -+ r with the signed radius
+// (sphere.rs:54-60), rect +-BBOX_WIDTH on its normal axis (rect.rs:82-99), RectBox min/max
+// (rect.rs:158-163).
+__device__ __forceinline__ void leaf_box(const DPrim& pr, double* b) {
+  const double* p = pr.p;
+  switch (pr.kind) {
+    case kPrimSphere:
+      b[0] = p[0] - p[3]; b[1] = p[1] - p[3]; b[2] = p[2] - p[3];
+      b[3] = p[0] + p[3]; b[4] = p[1] + p[3]; b[5] = p[2] + p[3];
+      break;
+    case kPrimRectXY:
+      b[0] = p[0]; b[1] = p[2]; b[2] = p[4] - 0.0001; b[3] = p[1]; b[4] = p[3]; b[5] = p[4] + 0.0001;
+      break;
+    case kPrimRectYZ:
+      b[0] = p[4] - 0.0001; b[1] = p[0]; b[2] = p[2]; b[3] = p[4] + 0.0001; b[4] = p[1]; b[5] = p[3];
+      break;
+    case kPrimRectXZ:
+      b[0] = p[0]; b[1] = p[4] - 0.0001; b[2] = p[2]; b[3] = p[1]; b[4] = p[4] + 0.0001; b[5] = p[3];
+      break;
+    default:
+      for (int k = 0; k < 6; ++k) b[k] = p[k];
+  }
+}
+
+// The hit leaf children of a 4-wide node against the running closest, each exactly as
+// bbox_tree.rs:60-71 does: f64 hit2 on the object's own bounding box, then the object.  Sphere
+// leaves first in their own loop (sphere.rs:28-46 only), then rect / box leaves, each in child order:
+// a wave runs the rect / box code only when one of its lanes holds such a leaf.
 template <int MODE>
-__device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, double a,
-                                            double t_min, bool h0, bool h1, bool h2, bool h3, int c0, int c1,
+__device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
+                                            RaySigns ns, double a, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, double& t_best, int& best, int& face_best,
                                             unsigned& ptests) {
-  auto kind = [](bool h, int c, unsigned bit, unsigned& sph, unsigned& gen) {
-    if (h && c < 0) {
-      if ((~c) & kLeafGeneric) gen |= bit;
-      else sph |= bit;
-    }
-  };
   unsigned sph = 0, gen = 0;
-  kind(h0, c0, 1u, sph, gen);
-  kind(h1, c1, 2u, sph, gen);
-  kind(h2, c2, 4u, sph, gen);
-  kind(h3, c3, 8u, sph, gen);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3;
+    if (lm & (1u << k)) {
+      if ((~c) & kLeafGeneric) gen |= 1u << k;
+      else sph |= 1u << k;
+    }
+  }
 #pragma unroll 1
   while (sph) {
     const int k = __builtin_ctz(sph);
     sph &= sph - 1;
     const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-    double t;
+    const double r = pr.p[3];
+    const double b[6] = {pr.p[0] - r, pr.p[1] - r, pr.p[2] - r, pr.p[0] + r, pr.p[1] + r, pr.p[2] + r};
+    double te, t;
+    if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
     ++ptests;
     if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; }
   }
@@ -492,7 +561,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     gen &= gen - 1;
     const int leaf = (~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3)) & (kLeafGeneric - 1);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-    double t;
+    double b[6], te, t;
+    leaf_box(pr, b);
+    if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
     int f = -1;
     ++ptests;
     if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; }
@@ -500,9 +571,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
 }
 
 // compare-exchange of (key, node) pairs: ascending key
-__device__ __forceinline__ void cas(double& ka, int& na, double& kb, int& nb) {
+__device__ __forceinline__ void cas(float& ka, int& na, float& kb, int& nb) {
   const bool sw = kb < ka;
-  const double k = sw ? kb : ka;
+  const float k = sw ? kb : ka;
   const int n = sw ? nb : na;
   kb = sw ? ka : kb;
   nb = sw ? na : nb;
@@ -510,13 +581,55 @@ __device__ __forceinline__ void cas(double& ka, int& na, double& kb, int& nb) {
   na = n;
 }
 
-// Closest hit over the 4-wide tree: the child boxes of a node are tested with the reference's f64
-// hit2, hit leaf children are tested at once in child order (they can shrink t_best), hit internal
-// children are visited nearest-first (the others pushed with their entry t; a popped entry beyond
-// t_best is skipped).  The exact boxes make every pruning decision one the reference's traversal
-// would also take, so the closest hit is the reference's (up to exact ties in t).
+// One node visit: conservative f32 tests of the four child boxes; hit leaf children tested exactly
+// at once (they can shrink t_best); hit internal children visited nearest-first (4-entry sorting
+// network on the f32 entry t), the others pushed with that lower bound and skipped on pop when
+// beyond the closest hit.  Returns the next node, or -1 when the traversal is complete.
 template <int STRIDE, int MODE>
-__device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
+__device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
+                                      v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
+                                      double& t_best, int& best, int& face_best, int& sp, int* stk_node,
+                                      float* stk_t, unsigned& visits, unsigned& ptests) {
+  const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
+  int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
+  const float tminf = __double2float_rd(t_min), tmaxf = __double2float_ru(t_best);
+  float k0 = node4_child(nd, 0, rf, o, inv, tminf, tmaxf, t_min, t_best);
+  float k1 = node4_child(nd, 1, rf, o, inv, tminf, tmaxf, t_min, t_best);
+  float k2 = node4_child(nd, 2, rf, o, inv, tminf, tmaxf, t_min, t_best);
+  float k3 = node4_child(nd, 3, rf, o, inv, tminf, tmaxf, t_min, t_best);
+  const float kInf = __builtin_inff();
+  visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
+  const unsigned lm = (k0 < kInf && c0 < 0 ? 1u : 0u) | (k1 < kInf && c1 < 0 ? 2u : 0u) |
+                      (k2 < kInf && c2 < 0 ? 4u : 0u) | (k3 < kInf && c3 < 0 ? 8u : 0u);
+  if (lm) leaf_tests4<MODE>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, best, face_best, ptests);
+  // internal children nearest-first: leaves, empty slots and misses sort last (key inf)
+  if (c0 < 0 || c0 == kEmptyChild) k0 = kInf;
+  if (c1 < 0 || c1 == kEmptyChild) k1 = kInf;
+  if (c2 < 0 || c2 == kEmptyChild) k2 = kInf;
+  if (c3 < 0 || c3 == kEmptyChild) k3 = kInf;
+  cas(k0, c0, k1, c1);
+  cas(k2, c2, k3, c3);
+  cas(k0, c0, k2, c2);
+  cas(k1, c1, k3, c3);
+  cas(k1, c1, k2, c2);
+  const double tb = t_best;
+  if (k3 < kInf && (double)k3 <= tb) { stk_node[sp * STRIDE] = c3; stk_t[sp * STRIDE] = k3; ++sp; }
+  if (k2 < kInf && (double)k2 <= tb) { stk_node[sp * STRIDE] = c2; stk_t[sp * STRIDE] = k2; ++sp; }
+  if (k1 < kInf && (double)k1 <= tb) { stk_node[sp * STRIDE] = c1; stk_t[sp * STRIDE] = k1; ++sp; }
+  if (k0 < kInf && (double)k0 <= tb) return c0;
+  while (sp > 0) {
+    --sp;
+    // a pushed subtree whose (lower-bound) entry lies beyond the current closest hit cannot hold it
+    if ((double)stk_t[sp * STRIDE] <= tb) return stk_node[sp * STRIDE];
+  }
+  return -1;
+}
+
+// Whole closest-hit query over the 4-wide tree.  The conservative internal tests and the exact
+// leaf tests make the set of primitives that can win the reference's (see DNode4F); the closest hit
+// is the reference's up to exact ties in t.
+template <int STRIDE, int MODE>
+__device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                          double t_min,
                                          double& t_best, int& face_best, int* stk_node, float* stk_t,
                                          unsigned& visits, unsigned& ptests
@@ -526,76 +639,36 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4* lds_node
                                          ) {
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   const RaySigns ns = ray_signs(inv);
+  const RayF rf = ray_f(S, o, inv);
   const double a = len2(d);
   int best = -1;
   int sp = 0;
   int node = 0;  // top node: child[0] = root
-  const double kInf = __builtin_inf();
   // a tree traversal visits every node at most once: more steps than nodes can only be a defect,
   // and ends the loop instead of hanging the wave
-  for (int steps = 0; steps < S.n_nodes4; ++steps) {
+  for (int steps = 0; steps < S.n_nodes4 && node >= 0; ++steps) {
 #ifdef RT_PHASE_TIMING
     ++g_trav_lane_steps;
 #endif
-    const DNode4& nd = fetch_node4<MODE>(S, lds_nodes, node);
-    int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
-    double k0 = kInf, k1 = kInf, k2 = kInf, k3 = kInf;
-    double te;
-    const bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, inv, ns, t_min, t_best, te);
-    if (h0) k0 = te;
-    const bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, inv, ns, t_min, t_best, te);
-    if (h1) k1 = te;
-    const bool h2 = (c2 != kEmptyChild) && slab_s(nd.box[2], o, inv, ns, t_min, t_best, te);
-    if (h2) k2 = te;
-    const bool h3 = (c3 != kEmptyChild) && slab_s(nd.box[3], o, inv, ns, t_min, t_best, te);
-    if (h3) k3 = te;
-    visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
-    // hit leaf children: spheres in a tight loop, then rects / boxes
-    leaf_tests4<MODE>(S, lds_prims, o, d, a, t_min, h0, h1, h2, h3, c0, c1, c2, c3, t_best, best, face_best, ptests);
-    // internal children nearest-first: leaves and misses sort last (key inf)
-    if (c0 < 0) k0 = kInf;
-    if (c1 < 0) k1 = kInf;
-    if (c2 < 0) k2 = kInf;
-    if (c3 < 0) k3 = kInf;
-    cas(k0, c0, k1, c1);
-    cas(k2, c2, k3, c3);
-    cas(k0, c0, k2, c2);
-    cas(k1, c1, k3, c3);
-    cas(k1, c1, k2, c2);
-    // a hit box has a finite entry t, so key < inf marks exactly the hit internal children (t_best
-    // itself may still be inf)
-    if (k3 < kInf && k3 <= t_best) { stk_node[sp * STRIDE] = c3; stk_t[sp * STRIDE] = __double2float_rd(k3); ++sp; }
-    if (k2 < kInf && k2 <= t_best) { stk_node[sp * STRIDE] = c2; stk_t[sp * STRIDE] = __double2float_rd(k2); ++sp; }
-    if (k1 < kInf && k1 <= t_best) { stk_node[sp * STRIDE] = c1; stk_t[sp * STRIDE] = __double2float_rd(k1); ++sp; }
-    if (k0 < kInf && k0 <= t_best) {
-      node = c0;
-    } else {
-      node = -1;
-      while (sp > 0) {
-        --sp;
-        if ((double)stk_t[sp * STRIDE] <= t_best) {
-          node = stk_node[sp * STRIDE];
-          break;
-        }
-      }
-      if (node < 0) break;
-    }
+    node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, best, face_best,
+                                sp, stk_node, stk_t, visits, ptests);
   }
   return best;
 }
 
-// One node visit of the 4-wide traversal (the body of traverse4's loop) for the postponed-shading
-// megakernel, where a ray's traversal state lives across other lanes' shading.
+// Step-wise form for wf_extend4, where a ray's traversal state lives across loop iterations.
 struct Trav4 {
   v3 inv;
   double a, t_best;
   int best, face, node, sp, steps;
   RaySigns ns;
+  RayF rf;
 };
 
-__device__ __forceinline__ void trav4_begin(Trav4& T, v3 d, double t_max) {
+__device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 d, double t_max) {
   T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   T.ns = ray_signs(T.inv);
+  T.rf = ray_f(S, o, T.inv);
   T.a = len2(d);
   T.t_best = t_max;
   T.best = -1;
@@ -607,62 +680,21 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, v3 d, double t_max) {
 
 // Returns true when the traversal is complete (T.best / T.t_best / T.face hold the closest hit).
 template <int STRIDE, int MODE>
-__device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4* lds_nodes, const DPrim* lds_prims, v3 o,
+__device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o,
                                            v3 d, double t_min, Trav4& T, int* stk_node, float* stk_t,
                                            unsigned& visits, unsigned& ptests) {
-  if (++T.steps > S.n_nodes4) return true;  // defect guard (a traversal visits each node at most once)
-  const double kInf = __builtin_inf();
-  const DNode4& nd = fetch_node4<MODE>(S, lds_nodes, T.node);
-  int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
-  double k0 = kInf, k1 = kInf, k2 = kInf, k3 = kInf;
-  double te;
-  const bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, T.inv, T.ns, t_min, T.t_best, te);
-  if (h0) k0 = te;
-  const bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, T.inv, T.ns, t_min, T.t_best, te);
-  if (h1) k1 = te;
-  const bool h2 = (c2 != kEmptyChild) && slab_s(nd.box[2], o, T.inv, T.ns, t_min, T.t_best, te);
-  if (h2) k2 = te;
-  const bool h3 = (c3 != kEmptyChild) && slab_s(nd.box[3], o, T.inv, T.ns, t_min, T.t_best, te);
-  if (h3) k3 = te;
-  visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
-  leaf_tests4<MODE>(S, lds_prims, o, d, T.a, t_min, h0, h1, h2, h3, c0, c1, c2, c3, T.t_best, T.best, T.face, ptests);
-  if (c0 < 0) k0 = kInf;
-  if (c1 < 0) k1 = kInf;
-  if (c2 < 0) k2 = kInf;
-  if (c3 < 0) k3 = kInf;
-  cas(k0, c0, k1, c1);
-  cas(k2, c2, k3, c3);
-  cas(k0, c0, k2, c2);
-  cas(k1, c1, k3, c3);
-  cas(k1, c1, k2, c2);
-  const double tb = T.t_best;
-  int sp = T.sp;
-  if (k3 < kInf && k3 <= tb) { stk_node[sp * STRIDE] = c3; stk_t[sp * STRIDE] = __double2float_rd(k3); ++sp; }
-  if (k2 < kInf && k2 <= tb) { stk_node[sp * STRIDE] = c2; stk_t[sp * STRIDE] = __double2float_rd(k2); ++sp; }
-  if (k1 < kInf && k1 <= tb) { stk_node[sp * STRIDE] = c1; stk_t[sp * STRIDE] = __double2float_rd(k1); ++sp; }
-  if (k0 < kInf && k0 <= tb) {
-    T.node = c0;
-    T.sp = sp;
-    return false;
-  }
-  while (sp > 0) {
-    --sp;
-    if ((double)stk_t[sp * STRIDE] <= tb) {
-      T.node = stk_node[sp * STRIDE];
-      T.sp = sp;
-      return false;
-    }
-  }
-  T.sp = 0;
-  return true;
+  if (++T.steps > S.n_nodes4) return true;  // defect guard
+  T.node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
+                                T.best, T.face, T.sp, stk_node, stk_t, visits, ptests);
+  return T.node < 0;
 }
 
 template <int MODE>
-__device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4* lds_nodes, DPrim* lds_prims) {
+__device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4F* lds_nodes, DPrim* lds_prims) {
   if (MODE == kNodesGlobal) return;
   const int4* src = reinterpret_cast<const int4*>(S.nodes4);
   int4* dst = reinterpret_cast<int4*>(lds_nodes);
-  const int n16 = S.n_lds_nodes4 * (int)(sizeof(DNode4) / 16);
+  const int n16 = S.n_lds_nodes4 * (int)(sizeof(DNode4F) / 16);
   for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
   if (MODE == kSceneLds) {
     const int4* ps = reinterpret_cast<const int4*>(S.prims);

@@ -31,16 +31,22 @@ struct alignas(16) DNode {
 };
 static_assert(sizeof(DNode) == 112, "DNode layout");
 
-// 4-wide node of the collapsed tree used by the megakernel (fewer dependent node fetches per ray);
-// same exact f64 child boxes and child encoding as DNode, except that a leaf child that is not a
-// sphere carries kLeafGeneric in its primitive index (~(prim | kLeafGeneric)), so traversal can test
-// sphere leaves in a tight loop and rects / boxes in a second one without loading the primitive first.
+// 4-wide node of the collapsed tree (megakernel, wf_extend4): child boxes in f32, SoA [axis][child],
+// inflated by the scene's inflation distance and rounded outward, so an f32 slab test on them accepts
+// a superset of what the reference's f64 Aabb::hit2 accepts on the exact box.  That is all an
+// internal level needs: the reference's test is monotone in the box planes and a parent's planes
+// are its children's, so whenever the reference passes a leaf's box it passes every enclosing box
+// too — internal tests never decide which primitives are tested; leaf tests do, and those run
+// exactly (f64 hit2 on the leaf's own bounding box, recomputed from the primitive).
+// child >= 0: node index; child < 0: leaf ~(prim | kLeafGeneric when not a sphere), so traversal can
+// test sphere leaves in a tight loop and rects / boxes in a second one; kEmptyChild: none.
 constexpr int32_t kLeafGeneric = 1 << 29;
-struct alignas(16) DNode4 {
-  double box[4][6];
+struct alignas(16) DNode4F {
+  float lo[3][4];  // lo[axis][child]
+  float hi[3][4];
   int32_t child[4];
 };
-static_assert(sizeof(DNode4) == 208, "DNode4 layout");
+static_assert(sizeof(DNode4F) == 112, "DNode4F layout");
 
 // Where a kernel instance reads BVH nodes from (template parameter of the traversal):
 enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2,
@@ -95,11 +101,13 @@ struct DScene {
   int32_t n_nodes, n_prims;
   int32_t stack_depth;     // max stack entries a traversal can need
   int32_t n_lds_nodes;     // nodes [0, n_lds_nodes) are copied into LDS per block (BFS order: top levels)
-  const DNode4* nodes4;    // the same tree collapsed to 4-wide nodes (node 0 = top node)
+  const DNode4F* nodes4;   // the same tree collapsed to 4-wide f32 nodes (node 0 = top node)
   int32_t n_nodes4;
   int32_t stack_depth4;    // exact worst-case stack of the 4-wide traversal
   int32_t n_lds_nodes4;    // 4-wide nodes [0, n_lds_nodes4) copied into LDS per megakernel block
   int32_t n_lds_prims;     // 0, or n_prims when the megakernel block also keeps the primitives in LDS
+  float origin_limit;      // rays with max|o| <= origin_limit take the f32 node test (its error bound
+                           // assumes it); others evaluate the same inflated boxes in f64
   int32_t sky;
   double sky_color[3];
 };

@@ -36,9 +36,9 @@ template <int THREADS, int MODE>
 __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
-  DNode4* lds_nodes = reinterpret_cast<DNode4*>(lds_raw);
-  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4));
-  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4) +
+  DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
                             (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) : 0);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
   float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
@@ -322,10 +322,10 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
-// megakernel block LDS: [n_lds_nodes4 x DNode4][n_lds_prims x DPrim][stack_depth4 x threads int]
+// megakernel block LDS: [n_lds_nodes4 x DNode4F][n_lds_prims x DPrim][stack_depth4 x threads int]
 // [stack_depth4 x threads float]
 size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int stack_depth4, int threads) {
-  return (size_t)n_lds_nodes4 * sizeof(DNode4) + (size_t)n_lds_prims * sizeof(DPrim) + (size_t)stack_depth4 * threads * 8;
+  return (size_t)n_lds_nodes4 * sizeof(DNode4F) + (size_t)n_lds_prims * sizeof(DPrim) + (size_t)stack_depth4 * threads * 8;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 

@@ -140,9 +140,9 @@ template <int THREADS>
 __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
-  DNode4* lds_nodes = reinterpret_cast<DNode4*>(lds_raw);
-  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4));
-  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4) +
+  DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
                             (size_t)P.scene.n_lds_prims * sizeof(DPrim);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
   float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   uint8_t nstate = 0;
   v3 o = V(0, 0, 0), d = V(0, 0, 0), no = V(0, 0, 0), nd = V(0, 0, 0);
   Trav4 T;
-  trav4_begin(T, V(1.0, 1.0, 1.0), 0.0);
+  trav4_begin(T, S, V(0.0, 0.0, 0.0), V(1.0, 1.0, 1.0), 0.0);
   unsigned visits = 0, ptests = 0, rays = 0;
   for (;;) {
     // A. a lane without a ray takes its prefetched one (if that slot holds a ray)
@@ -170,7 +170,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
         slot = nslot;
         o = no;
         d = nd;
-        trav4_begin(T, d, __builtin_inf());
+        trav4_begin(T, S, o, d, __builtin_inf());
         active = true;
         ++rays;
       }
@@ -570,7 +570,7 @@ static int wf_mode(const DScene& S) {
 }
 
 size_t wf_extend4_lds(const DScene& S) {
-  return (size_t)S.n_lds_nodes4 * sizeof(DNode4) + (size_t)S.n_lds_prims * sizeof(DPrim) +
+  return (size_t)S.n_lds_nodes4 * sizeof(DNode4F) + (size_t)S.n_lds_prims * sizeof(DPrim) +
          (size_t)S.stack_depth4 * kTraceThreadsWide * 8;
 }
 
