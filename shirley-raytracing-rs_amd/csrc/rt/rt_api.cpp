@@ -18,7 +18,7 @@
 #include "rt_layout.h"
 
 namespace rt {
-size_t trace_lds_bytes(int n_lds_nodes, int stack_depth, int threads);
+size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads);
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
@@ -861,6 +861,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const bool prims_lds = wide && wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) <= kLdsBytes &&
                          !getenv("SHIRLEY_NO_LDS_PRIMS");
   S.n_lds_prims = prims_lds ? d->n_objects : 0;
+  // and the Perlin tables (marble's ~210 gathers per evaluation from LDS)
+  const bool perlin_lds = prims_lds && d->n_perlin > 0 &&
+                          wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) +
+                                  (long long)d->n_perlin * (long long)sizeof(DPerlin) <= kLdsBytes &&
+                          !getenv("SHIRLEY_NO_LDS_PERLIN");
+  S.n_lds_perlin = perlin_lds ? d->n_perlin : 0;
 
   int bpc = 0;
   HIP_TRY(c, trace_occupancy(S, c->mk_threads, &bpc));

@@ -701,6 +701,11 @@ __device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4F* lds_nodes
     int4* pd = reinterpret_cast<int4*>(lds_prims);
     const int p16 = S.n_lds_prims * (int)(sizeof(DPrim) / 16);
     for (int i = threadIdx.x; i < p16; i += blockDim.x) pd[i] = ps[i];
+    // Perlin tables right after the primitives (when they fit: S.n_lds_perlin > 0)
+    const int4* ts = reinterpret_cast<const int4*>(S.perlin);
+    int4* td = reinterpret_cast<int4*>(lds_prims + S.n_lds_prims);
+    const int t16 = S.n_lds_perlin * (int)(sizeof(DPerlin) / 16);
+    for (int i = threadIdx.x; i < t16; i += blockDim.x) td[i] = ts[i];
   }
   __syncthreads();
 }
@@ -733,7 +738,8 @@ __device__ __forceinline__ int32_t sat_i32(double x) {
 // are exactly `1 - uu` and `uu`: uu = u*u*(3-2u) lies in [0, 1] for u in [0, 1) (it rounds to at
 // most 1.0), so 0*uu and 0*(1-uu) are +0, 1*x is x and x + 0 is x; for a NaN u both forms are NaN.
 // So the value is bit-identical with a third of the reference's arithmetic.
-__device__ __forceinline__ double perlin_noise_inl(const DPerlin* T, v3 p) {
+template <class TP>  // table pointer: const DPerlin* (global) or LdsPerlin* (LDS)
+__device__ __forceinline__ double perlin_noise_t(TP T, v3 p) {
   double xf = floor(p.x), yf = floor(p.y), zf = floor(p.z);
   double u = p.x - xf, v = p.y - yf, w = p.z - zf;
   uint32_t i = (uint32_t)sat_i32(xf), j = (uint32_t)sat_i32(yf), k = (uint32_t)sat_i32(zf);
@@ -763,19 +769,24 @@ __device__ __forceinline__ double perlin_noise_inl(const DPerlin* T, v3 p) {
   return accum;
 }
 
-__device__ __noinline__ double perlin_noise(const DPerlin* T, v3 p) { return perlin_noise_inl(T, p); }
+__device__ __forceinline__ double perlin_noise_inl(const DPerlin* T, v3 p) { return perlin_noise_t(T, p); }
+__device__ __noinline__ double perlin_noise(const DPerlin* T, v3 p) { return perlin_noise_t(T, p); }
+
+// A Perlin table in LDS, typed so that out-of-line code reads it with ds_read (a generic pointer
+// would make every gather a FLAT load).
+typedef __attribute__((address_space(3))) const DPerlin LdsPerlin;
 
 // perlin/mod.rs:162-183 NoiseTexture::value ("marble"): 0.5 (1 + sin(scale p.z + 10 turb(p, 7)));
 // the x/y terms of the reference's dot with (0,0,1) contribute exactly 0.  NOISE = the octave's
 // noise function (out-of-line in the megakernel to hold its registers, inline in wf_texture).
-template <double (*NOISE)(const DPerlin*, v3)>
-__device__ __forceinline__ double marble_impl(const DPerlin* T, double sc, v3 p) {
+template <class TP>
+__device__ __forceinline__ double marble_t(TP T, double sc, v3 p) {
   double accum = 0.0;
   v3 tp = p;
   double weight = 1.0;
 #pragma unroll 1
   for (int i = 0; i < 7; ++i) {  // turbulence, perlin/mod.rs:111-124
-    accum += weight * NOISE(T, tp);
+    accum += weight * perlin_noise_t(T, tp);
     weight *= 0.5;
     tp = scale(tp, 2.0);
   }
@@ -784,14 +795,10 @@ __device__ __forceinline__ double marble_impl(const DPerlin* T, double sc, v3 p)
   return 0.5 * (1.0 + total_noise);
 }
 
-#ifndef RT_MARBLE_NOISE
-#define RT_MARBLE_NOISE perlin_noise_inl  // octave noise inside the out-of-line marble (perlin_noise: a call per octave)
-#endif
-__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) { return marble_impl<RT_MARBLE_NOISE>(T, sc, p); }
-
-__device__ __forceinline__ double marble_inl(const DPerlin* T, double sc, v3 p) {
-  return marble_impl<perlin_noise_inl>(T, sc, p);
-}
+// out of line in the megakernel (holds its register budget), inline in wf_texture
+__device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) { return marble_t(T, sc, p); }
+__device__ __noinline__ double marble_lds(LdsPerlin* T, double sc, v3 p) { return marble_t(T, sc, p); }
+__device__ __forceinline__ double marble_inl(const DPerlin* T, double sc, v3 p) { return marble_t(T, sc, p); }
 
 // checker.rs:28-30
 __device__ __noinline__ double checker_sines(double s, double x, double y, double z) {
@@ -871,12 +878,15 @@ __device__ __forceinline__ UV hit_uv(const DPrim& pr, int face, const Hit& h) {
 
 // Texture value at a hit (texture.rs Texture::value): checker resolved by the hit point, Perlin
 // marble by the hit point, solid directly, image by u, v (computed only for an image leaf).
-__device__ __forceinline__ v3 texture_value(const DScene& S, int ti, int prim, int face, const Hit& h) {
+// `lds_perlin`: the block's LDS copy of the Perlin tables, or null (tables read through L1/L2).
+__device__ __forceinline__ v3 texture_value(const DScene& S, const DPerlin* lds_perlin, int ti, int prim, int face,
+                                            const Hit& h) {
   const int leaf = resolve_texture(S, ti, h.point);
   const DTex& tx = S.texs[leaf];
   if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);  // solid.rs:17-21
   if (tx.kind == RT_TEX_PERLIN) {
-    double n = marble(S.perlin + tx.table, tx.scale, h.point);
+    const double n = lds_perlin ? marble_lds((LdsPerlin*)(lds_perlin + tx.table), tx.scale, h.point)
+                                : marble(S.perlin + tx.table, tx.scale, h.point);
     return V(n, n, n);
   }
   const UV uv = hit_uv(S.prims[prim], face, h);
@@ -921,10 +931,10 @@ __device__ __forceinline__ v3 sky(const DScene& S, v3 d) {
 // random_in_unit_sphere (metal.rs:32, lambertian.rs:23 via random_unit_vector); it has one call site.
 // The hit record comes without u, v (prim_record<false>); (prim, face, t) let an image texture
 // rebuild them.
-__device__ __forceinline__ bool shade(const DScene& S, const DMat& m, Rng& rng, uint64_t seed, v3& o, v3& d,
-                                      const Hit& h, int prim, int face, v3& att, v3& em) {
+__device__ __forceinline__ bool shade(const DScene& S, const DPerlin* lds_perlin, const DMat& m, Rng& rng,
+                                      uint64_t seed, v3& o, v3& d, const Hit& h, int prim, int face, v3& att, v3& em) {
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
-    v3 e = texture_value(S, m.tex, prim, face, h);
+    v3 e = texture_value(S, lds_perlin, m.tex, prim, face, h);
     em = em + hmul(att, e);
     return false;
   }
@@ -948,7 +958,7 @@ __device__ __forceinline__ bool shade(const DScene& S, const DMat& m, Rng& rng, 
     return true;
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
-  v3 a = texture_value(S, m.tex, prim, face, h);
+  v3 a = texture_value(S, lds_perlin, m.tex, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
     double s = dot(h.normal, scale(d, -1.0));
     em = em + hmul(att, scale(a, s / len(d)));

@@ -106,6 +106,7 @@ struct DScene {
   int32_t stack_depth4;    // exact worst-case stack of the 4-wide traversal
   int32_t n_lds_nodes4;    // 4-wide nodes [0, n_lds_nodes4) copied into LDS per megakernel block
   int32_t n_lds_prims;     // 0, or n_prims when the megakernel block also keeps the primitives in LDS
+  int32_t n_lds_perlin;    // 0, or n_perlin when the megakernel block also keeps the Perlin tables in LDS
   float origin_limit;      // rays with max|o| <= origin_limit take the f32 node test (its error bound
                            // assumes it); others evaluate the same inflated boxes in f64
   int32_t sky;

@@ -38,8 +38,13 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
   const int tid = threadIdx.x;
   DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
   DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
+  const DPerlin* lds_perlin = (MODE == kSceneLds && P.scene.n_lds_perlin > 0)
+                                  ? reinterpret_cast<const DPerlin*>(lds_prims + P.scene.n_lds_prims)
+                                  : nullptr;
   unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
-                            (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) : 0);
+                            (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) +
+                                                     (size_t)P.scene.n_lds_perlin * sizeof(DPerlin)
+                                               : 0);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
   float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
   stage_nodes4<MODE>(P.scene, lds_nodes, lds_prims);
@@ -170,7 +175,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
         Hit h;
         prim_record<false>(pr, face, o, d, t_best, h);
         const DMat m = S.mats[pr.material];
-        alive = shade(S, m, rng, seed, o, d, h, prim, face, att, em);
+        alive = shade(S, lds_perlin, m, rng, seed, o, d, h, prim, face, att, em);
       } else {
         em = em + hmul(att, sky(S, d));
         alive = false;
@@ -324,8 +329,9 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
 // ------------------------------------------------------------------------------------------
 // megakernel block LDS: [n_lds_nodes4 x DNode4F][n_lds_prims x DPrim][stack_depth4 x threads int]
 // [stack_depth4 x threads float]
-size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int stack_depth4, int threads) {
-  return (size_t)n_lds_nodes4 * sizeof(DNode4F) + (size_t)n_lds_prims * sizeof(DPrim) + (size_t)stack_depth4 * threads * 8;
+size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads) {
+  return (size_t)n_lds_nodes4 * sizeof(DNode4F) + (size_t)n_lds_prims * sizeof(DPrim) +
+         (size_t)n_lds_perlin * sizeof(DPerlin) + (size_t)stack_depth4 * threads * 8;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 
@@ -339,7 +345,7 @@ static int node_mode4(const DScene& S) {
 template <int THREADS, int MODE>
 static hipError_t occupancy_impl(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
-  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.n_lds_prims, S.stack_depth4, THREADS);
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.n_lds_prims, S.n_lds_perlin, S.stack_depth4, THREADS);
   hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -373,7 +379,7 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
 }
 
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
-  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.n_lds_prims, p.scene.stack_depth4, threads);
+  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads);
   if (threads == kTraceThreadsWide) {
     if (p.scene.n_lds_prims > 0)
       hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kSceneLds>), dim3(blocks), dim3(threads), lds, stream, p);

@@ -143,7 +143,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
   DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
   unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
-                            (size_t)P.scene.n_lds_prims * sizeof(DPrim);
+                            (size_t)P.scene.n_lds_prims * sizeof(DPrim) + (size_t)P.scene.n_lds_perlin * sizeof(DPerlin);
   int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
   float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
   stage_nodes4<kSceneLds>(P.scene, lds_nodes, lds_prims);
@@ -571,7 +571,7 @@ static int wf_mode(const DScene& S) {
 
 size_t wf_extend4_lds(const DScene& S) {
   return (size_t)S.n_lds_nodes4 * sizeof(DNode4F) + (size_t)S.n_lds_prims * sizeof(DPrim) +
-         (size_t)S.stack_depth4 * kTraceThreadsWide * 8;
+         (size_t)S.n_lds_perlin * sizeof(DPerlin) + (size_t)S.stack_depth4 * kTraceThreadsWide * 8;
 }
 
 // The 4-wide, scene-in-LDS extend kernel for scenes where the megakernel runs wide (`S` = that scene).
