@@ -242,6 +242,10 @@ int rt_bvh_build_host(const rt_scene_desc* scene, int32_t bvh_builder, int32_t* 
 /* Output stage on the host, exactly image::to_image (image.rs:31-44) + Color::to_pixel (color.rs:31-38):
  * c/samples -> sqrt -> (x*255.999) saturating to u8, row j -> output row H-1-j.  rgb8: [H][W][3], row 0 = top. */
 int rt_tonemap(const double* accum, int32_t width, int32_t height, int32_t samples, uint8_t* rgb8);
+/* The same on the device: accum_dev [H][W][3] sums -> rgb8_dev [H][W][3] with
+ * row 0 = top, on `stream` (NULL: the context's stream), asynchronous.  Bit-identical to rt_tonemap. */
+int rt_tonemap_device(rt_ctx* ctx, const double* accum_dev, int32_t width, int32_t height, int32_t samples,
+                      uint8_t* rgb8_dev, void* stream);
 
 #ifdef __cplusplus
 }

@@ -19,6 +19,8 @@
 #include <string>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "../../../include/shirley_host.h"
 #include "../../../include/shirley_rt.h"
 
@@ -72,12 +74,37 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
   p.tile_rank = 0;
   p.tile_world = 1;
   p.sample_chunk = a.sample_chunk;
-  std::vector<double> accum((size_t)cam.image_width * cam.image_height * 3);
+  const size_t n = (size_t)cam.image_width * cam.image_height * 3;
+  std::vector<double> accum;
+  std::vector<uint8_t> rgb(n);
   auto t1 = std::chrono::steady_clock::now();
-  if ((st = rt_render(ctx, &cam, &p, accum.data()))) {
-    std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
-    rt_destroy(ctx);
-    return 1;
+  if (!a.dump_accum.empty()) {  // the raw sums are wanted on the host: render + host tonemap
+    accum.resize(n);
+    if ((st = rt_render(ctx, &cam, &p, accum.data()))) {
+      std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
+      rt_destroy(ctx);
+      return 1;
+    }
+    rt_tonemap(accum.data(), cam.image_width, cam.image_height, samples, rgb.data());  // image.rs:31-44
+  } else {  // sums stay in HBM; to_image runs on the device and only RGB8 crosses PCIe
+    double* acc_dev = nullptr;
+    uint8_t* rgb_dev = nullptr;
+    if (hipMalloc((void**)&acc_dev, n * sizeof(double)) != hipSuccess || hipMalloc((void**)&rgb_dev, n) != hipSuccess) {
+      std::fprintf(stderr, "error: device allocation of the image failed\n");
+      rt_destroy(ctx);
+      return 1;
+    }
+    st = rt_render_device(ctx, &cam, &p, acc_dev, nullptr);
+    if (!st) st = rt_tonemap_device(ctx, acc_dev, cam.image_width, cam.image_height, samples, rgb_dev, nullptr);
+    if (!st) st = rt_synchronize(ctx);
+    if (!st && hipMemcpy(rgb.data(), rgb_dev, n, hipMemcpyDeviceToHost) != hipSuccess) st = RT_E_HIP;
+    (void)hipFree(acc_dev);
+    (void)hipFree(rgb_dev);
+    if (st) {
+      std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
+      rt_destroy(ctx);
+      return 1;
+    }
   }
   auto t2 = std::chrono::steady_clock::now();
   rt_counters cnt{};
@@ -94,8 +121,6 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
     std::ofstream f(a.dump_accum, std::ios::binary);
     f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
   }
-  std::vector<uint8_t> rgb(accum.size());
-  rt_tonemap(accum.data(), cam.image_width, cam.image_height, samples, rgb.data());  // image.rs:31-44
   if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
     std::fprintf(stderr, "error: %s\n", sh_last_error());
     return 1;

@@ -23,6 +23,7 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
                          int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
+hipError_t launch_tonemap(const double* accum, int width, int height, double inv, uint8_t* rgb8, hipStream_t stream);
 hipError_t launch_unpack(const double* gathered, int world, int max_tiles, int n_tiles_total, int tiles_x, int width,
                          int height, double* out, hipStream_t stream);
 hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, double t_max, void* out,
@@ -1089,6 +1090,17 @@ int rt_tonemap(const double* accum, int32_t width, int32_t height, int32_t sampl
         o[k] = (std::isnan(y) || y <= 0.0) ? 0 : (y >= 255.0 ? 255 : (uint8_t)y);
       }
     }
+  return RT_OK;
+}
+
+int rt_tonemap_device(rt_ctx* c, const double* accum_dev, int32_t width, int32_t height, int32_t samples,
+                      uint8_t* rgb8_dev, void* stream) {
+  if (!c || !accum_dev || !rgb8_dev || width < 1 || height < 1) return RT_E_INVALID;
+  hipStream_t s;
+  resolve_stream(c, stream, &s);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const double inv = 1.0 / (double)(samples == 0 ? 1 : samples);
+  HIP_TRY(c, launch_tonemap(accum_dev, width, height, inv, rgb8_dev, s));
   return RT_OK;
 }
 

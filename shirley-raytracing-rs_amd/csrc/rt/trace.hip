@@ -263,6 +263,19 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
   }
 }
 
+// image.rs:31-44 to_image + color.rs:31-38 to_pixel on the device: per channel c * (1/S), sqrt,
+// * 255.999 and Rust's saturating `as u8` (NaN -> 0); image row j becomes output row H-1-j.
+// One thread per output byte (coalesced stores).
+__global__ __launch_bounds__(256) void tonemap_kernel(const double* __restrict__ accum, int width, int height,
+                                                      double inv, uint8_t* __restrict__ rgb8) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)width * height * 3;
+  if (i >= n) return;
+  const long long row = i / ((long long)width * 3), rest = i - row * width * 3;
+  const double y = sqrt(accum[((long long)(height - 1 - row) * width) * 3 + rest] * inv) * 255.999;
+  rgb8[i] = (y != y || y <= 0.0) ? (uint8_t)0 : (y >= 255.0 ? (uint8_t)255 : (uint8_t)y);
+}
+
 // Scatter a gathered [world][max_tiles][64][3] buffer into the [H][W][3] image.
 __global__ __launch_bounds__(256) void unpack_kernel(const double* __restrict__ gathered, int world, int max_tiles,
                                                      int n_tiles_total, int tiles_x, int width, int height,
@@ -421,6 +434,14 @@ hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, 
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, stream, partial, n_chunks, n_tiles_rank, tiles_x,
                      ty0, tile_rank, tile_world, width, row0, row1, packed, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tonemap(const double* accum, int width, int height, double inv, uint8_t* rgb8, hipStream_t stream) {
+  const long long n = (long long)width * height * 3;
+  const int blocks = (int)((n + 255) / 256);
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(tonemap_kernel, dim3(blocks), dim3(256), 0, stream, accum, width, height, inv, rgb8);
   return hipGetLastError();
 }
 

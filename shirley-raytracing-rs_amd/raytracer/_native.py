@@ -123,6 +123,8 @@ RT_SIGNATURES = {
     "rt_bvh_build_host": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int32, C.POINTER(C.c_int32),
                                     C.POINTER(rt_bvh_node), C.POINTER(C.c_int32)]),
     "rt_tonemap": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
+    "rt_tonemap_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p,
+                                    C.c_void_p]),
 }
 
 # every symbol declared in include/shirley_host.h

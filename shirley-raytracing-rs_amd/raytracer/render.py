@@ -109,6 +109,12 @@ class Device:
                                                           C.c_void_p(gathered_ptr), C.c_void_p(accum_ptr),
                                                           C.c_void_p(stream or None)))
 
+    def tonemap_device(self, accum_ptr: int, width: int, height: int, samples: int, rgb8_ptr: int,
+                       stream: int = 0):
+        """rt_tonemap_device: device [H][W][3] f64 sums -> device RGB8, row 0 = top (to_image)."""
+        _check(self._h, N.rt_lib().rt_tonemap_device(self._h, C.c_void_p(accum_ptr), int(width), int(height),
+                                                     int(samples), C.c_void_p(rgb8_ptr), C.c_void_p(stream or None)))
+
     def hit(self, rays: np.ndarray, t_min: float = 0.001, t_max: float = float("inf")):
         """Closest hits for rays [n][6] (Hittable for Scene, scene/mod.rs:180-190) -> rt_hit array."""
         r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)

@@ -288,3 +288,53 @@ def test_full_size_rows_match_oracle(gpu, engine):
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), 200, 202)
     check_parity(rows, ora, spp)
     assert np.isfinite(full).all() and (full >= 0).all()
+
+
+def test_device_tonemap_matches_host(gpu):
+    """rt_tonemap_device (to_image on the GPU) == the host rt_tonemap, byte for
+    byte, on a rendered frame and on synthetic sums with NaN / negative / huge / tiny values."""
+    import torch
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    cam = rt.default_camera(48, "std16x9")
+    gpu.upload(scene)
+    spp = 3
+    frame = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED))
+    rng = np.random.default_rng(7)
+    synth = rng.uniform(-0.5, 4.0, size=frame.shape) * spp
+    flat = synth.reshape(-1)
+    flat[::97] = np.nan
+    flat[1::89] = np.inf
+    flat[2::83] = -np.inf
+    flat[3::79] = 5e-324
+    flat[4::73] = 0.0
+    flat[5::71] = -0.0
+    flat[6::67] = spp * (255.0 / 255.999) ** 2  # at the saturation edge
+    for accum, s in ((frame, spp), (synth, spp), (synth, 0)):
+        want = rt.to_image(accum, s)
+        dev = torch.from_numpy(np.ascontiguousarray(accum)).to("cuda")
+        out = torch.zeros(accum.shape, dtype=torch.uint8, device="cuda")
+        gpu.tonemap_device(dev.data_ptr(), accum.shape[1], accum.shape[0], s, out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_cli_render_device_output_stage(tmp_path):
+    """`ray-cli render random` end to end on the GPU: the default path (sums stay in HBM, to_image on
+    the device, RGB8 copied back) writes the same PNG as the host path (--dump-accum: f64 sums copied
+    back, host tonemap), and that PNG is to_image of the dumped sums."""
+    import os
+    import subprocess
+    from PIL import Image
+    from raytracer import _native as N
+    cli = os.path.join(N.BIN_DIR, "ray-cli")
+    common = ["render", "random", "-w", "96", "-s", "4", "--seed", "0x5EED", "--camera-aspect-ratio", "std16x9"]
+    a, b, acc = str(tmp_path / "dev.png"), str(tmp_path / "host.png"), str(tmp_path / "acc.f64")
+    r1 = subprocess.run([cli] + common + ["-o", a], capture_output=True, text=True)
+    assert r1.returncode == 0, r1.stderr
+    r2 = subprocess.run([cli] + common + ["-o", b, "--dump-accum", acc], capture_output=True, text=True)
+    assert r2.returncode == 0, r2.stderr
+    img_a, img_b = np.asarray(Image.open(a)), np.asarray(Image.open(b))
+    assert np.array_equal(img_a, img_b)
+    sums = np.fromfile(acc, dtype=np.float64).reshape(img_a.shape[0], img_a.shape[1], 3)
+    assert np.array_equal(rt.to_image(sums, 4), img_a)
