@@ -800,6 +800,63 @@ __device__ __noinline__ double marble(const DPerlin* T, double sc, v3 p) { retur
 __device__ __noinline__ double marble_lds(LdsPerlin* T, double sc, v3 p) { return marble_t(T, sc, p); }
 __device__ __forceinline__ double marble_inl(const DPerlin* T, double sc, v3 p) { return marble_t(T, sc, p); }
 
+__device__ __forceinline__ unsigned long long lanes_below() {
+  const unsigned lane = __lane_id();
+  return lane == 0 ? 0ull : (~0ull) >> (64 - lane);
+}
+
+// Lane of the j-th (0-based) set bit of `mask` (binary search on prefix popcounts).
+__device__ __forceinline__ int select_lane(unsigned long long mask, int j) {
+  int lo = 0;
+  for (int w = 32; w > 0; w >>= 1) {
+    const unsigned long long below = (lo + w >= 64) ? mask : (mask & ((1ull << (lo + w)) - 1ull));
+    if (__popcll(below) <= j) lo += w;
+  }
+  return lo;
+}
+
+// perlin/mod.rs:162-183 marble for every lane with `need`, computed by the whole wave: the k needing
+// lanes' 7 octaves are 7k work items (octave-major), dealt one per lane per round, so a wave needs
+// ceil(7k / 64) noise evaluations instead of 7 (the octave loop otherwise runs for all lanes while
+// any one needs it).  Octave i's input p * 2^i is the reference's tp after i doublings (scaling by 2 is
+// exact), its weight 0.5^i likewise, and each owner adds its octaves in the reference's order — the
+// value is bit-identical.  Must be called in wave-uniform control flow (it shuffles).
+template <class TP>
+__device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, double sc, v3 p) {
+  const unsigned long long mask = __ballot(need);
+  if (mask == 0ull) return 0.0;
+  const int k = __popcll(mask);
+  const int lane = __lane_id();
+  const int rank = __popcll(mask & lanes_below());
+  const int total = 7 * k;
+  double accum = 0.0;
+  for (int base = 0; base < total; base += 64) {
+    const int item = base + lane;
+    const bool valid = item < total;
+    const int oct = valid ? item / k : 0;
+    const int owner = select_lane(mask, valid ? item - oct * k : 0);
+    const double qx = __shfl(p.x, owner), qy = __shfl(p.y, owner), qz = __shfl(p.z, owner);
+    const int qt = __shfl(tab, owner);
+    double nv = 0.0;
+    if (valid) {
+      const double f = (double)(1 << oct);  // 2^oct, exact
+      nv = perlin_noise_t(tables + qt, V(qx * f, qy * f, qz * f));
+    }
+    // owners take their octaves of this round, in octave order
+    double w = 1.0;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const int my = i * k + rank;
+      const bool mine = need && my >= base && my < base + 64;
+      const double v = __shfl(nv, mine ? my - base : 0);
+      if (mine) accum += w * v;
+      w *= 0.5;
+    }
+  }
+  const double turb = 10.0 * fabs(accum);
+  return need ? 0.5 * (1.0 + sin(sc * p.z + turb)) : 0.0;
+}
+
 // checker.rs:28-30
 __device__ __noinline__ double checker_sines(double s, double x, double y, double z) {
   return sin(s * x) * sin(s * y) * sin(s * z);
@@ -878,6 +935,16 @@ __device__ __forceinline__ UV hit_uv(const DPrim& pr, int face, const Hit& h) {
 
 // Texture value at a hit (texture.rs Texture::value): checker resolved by the hit point, Perlin
 // marble by the hit point, solid directly, image by u, v (computed only for an image leaf).
+// Texture value of an already resolved leaf whose marble value (if Perlin) is `pn`.
+__device__ __forceinline__ v3 leaf_texture_value(const DScene& S, int leaf, double pn, int prim, int face,
+                                                 const Hit& h) {
+  const DTex& tx = S.texs[leaf];
+  if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);  // solid.rs:17-21
+  if (tx.kind == RT_TEX_PERLIN) return V(pn, pn, pn);
+  const UV uv = hit_uv(S.prims[prim], face, h);
+  return image_texel(S, tx, uv.u, uv.v);
+}
+
 // `lds_perlin`: the block's LDS copy of the Perlin tables, or null (tables read through L1/L2).
 __device__ __forceinline__ v3 texture_value(const DScene& S, const DPerlin* lds_perlin, int ti, int prim, int face,
                                             const Hit& h) {
@@ -959,6 +1026,50 @@ __device__ __forceinline__ bool shade(const DScene& S, const DPerlin* lds_perlin
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
   v3 a = texture_value(S, lds_perlin, m.tex, prim, face, h);
+  if (m.kind == RT_MAT_FAIRY_LIGHT) {
+    double s = dot(h.normal, scale(d, -1.0));
+    em = em + hmul(att, scale(a, s / len(d)));
+    a = unit(a);
+  }
+  v3 sc = h.normal + unit(r);
+  if (near_zero(sc)) sc = h.normal;
+  o = h.point;
+  d = sc;
+  att = hmul(att, a);
+  return true;
+}
+
+// shade() with the texture leaf already resolved and its marble value (if any) computed by the wave
+// (marble_coop); same steps otherwise.
+__device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, Rng& rng,
+                                          uint64_t seed, v3& o, v3& d, const Hit& h, int prim, int face, v3& att,
+                                          v3& em) {
+  if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
+    v3 e = leaf_texture_value(S, leaf, pn, prim, face, h);
+    em = em + hmul(att, e);
+    return false;
+  }
+  if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
+    double ratio = h.front_face ? (1.0 / m.param) : m.param;
+    v3 ud = unit(d);
+    double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
+    double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+    bool refl = ratio * sin_theta > 1.0;
+    if (!refl) refl = reflectance(cos_theta, ratio) > rng_next(rng, seed);  // drawn only if not TIR
+    o = h.point;
+    d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
+    return true;  // attenuation = Color::ones()
+  }
+  v3 r = random_in_unit_sphere(rng, seed);
+  if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
+    v3 reflected = reflect(unit(d), h.normal);
+    o = h.point;
+    d = reflected + scale(r, m.param);
+    att = hmul(att, V(m.albedo[0], m.albedo[1], m.albedo[2]));
+    return true;
+  }
+  // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
+  v3 a = leaf_texture_value(S, leaf, pn, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
     double s = dot(h.normal, scale(d, -1.0));
     em = em + hmul(att, scale(a, s / len(d)));

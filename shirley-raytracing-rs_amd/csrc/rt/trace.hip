@@ -154,28 +154,55 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     ph_regen += ph1 - ph0;
     const unsigned long long ph_before = ph_lane_steps;
 #endif
+    // (a) closest hit, hit record, and the texture leaf of a diffuse / emitting material
+    bool hit = false, need_pn = false;
+    int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0;
+    double t_best = __builtin_inf(), psc = 0.0;
+    Hit h;
+    h.point = V(0.0, 0.0, 0.0);
+    h.normal = h.point;
+    h.t = h.u = h.v = 0.0;
+    h.front_face = false;
+#ifdef RT_PHASE_TIMING
+    unsigned long long ph2 = ph1;
+#endif
     if (active) {
       ++n_seg;
-      double t_best = __builtin_inf();
-      int face = -1;
 #ifdef RT_PHASE_TIMING
-      int prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits,
-                                          ptests, ph_lane_steps);
-#else
-      int prim =
-          traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits, ptests);
-#endif
-#ifdef RT_PHASE_TIMING
-      const unsigned long long ph2 = clock64();
+      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits,
+                                      ptests, ph_lane_steps);
+      ph2 = clock64();
       ph_trav += ph2 - ph1;
+#else
+      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits,
+                                      ptests);
 #endif
-      bool alive;
       if (prim >= 0) {
+        hit = true;
         const DPrim pr = S.prims[prim];
-        Hit h;
         prim_record<false>(pr, face, o, d, t_best, h);
-        const DMat m = S.mats[pr.material];
-        alive = shade(S, lds_perlin, m, rng, seed, o, d, h, prim, face, att, em);
+        mat = pr.material;
+        const int mk = S.mats[mat].kind;
+        if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT) {
+          leaf = resolve_texture(S, S.mats[mat].tex, h.point);
+          const DTex& tx = S.texs[leaf];
+          if (tx.kind == RT_TEX_PERLIN) {
+            need_pn = true;
+            ptab = tx.table;
+            psc = tx.scale;
+          }
+        }
+      }
+    }
+    // (b) Perlin marble values for the lanes that need one, by the whole wave (wave-uniform)
+    const double pn = lds_perlin ? marble_coop((LdsPerlin*)lds_perlin, need_pn, ptab, psc, h.point)
+                                 : marble_coop(S.perlin, need_pn, ptab, psc, h.point);
+    // (c) emitted + scatter (render.rs:31-45) or the sky
+    if (active) {
+      bool alive;
+      if (hit) {
+        const DMat m = S.mats[mat];
+        alive = shade_pre(S, m, leaf, pn, rng, seed, o, d, h, prim, face, att, em);
       } else {
         em = em + hmul(att, sky(S, d));
         alive = false;
