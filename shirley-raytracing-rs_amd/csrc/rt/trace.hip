@@ -10,8 +10,11 @@
 //     64-unit window (ballot + popcount rank, one global atomic per 64 units);
 //   * units are enumerated tile-major (8x8 pixel tile x sample chunk x lane), so a fresh window
 //     hands a wave 64 neighbouring pixels: coherent primary rays;
-//   * BVH2 with both child boxes inline (112-B nodes), near-child-first traversal, per-lane
-//     stack in LDS laid out [depth][lane] (bank = lane % 32: conflict-free at any depth);
+//   * 4-wide collapsed BVH with conservative f32 child boxes (112-B DNode4F) and exact f64 leaf
+//     tests, nearest-first traversal, per-lane stack in LDS laid out [depth][lane] (conflict-free
+//     at any depth); for scenes that fit, the nodes, primitives and Perlin tables live in LDS too
+//     (one 768-thread block per CU);
+//   * Perlin marble octaves of a segment are dealt across the whole wave (marble_coop);
 //   * per-unit partial sums go to HBM once; a reduce kernel sums chunks in order (deterministic).
 #include "rt_device.h"
 
