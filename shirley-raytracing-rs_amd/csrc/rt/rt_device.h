@@ -476,28 +476,62 @@ __device__ __forceinline__ RayF ray_f(const DScene& S, v3 o, v3 inv) {
   return r;
 }
 
-// Conservative test of child k of a 4-wide node: entry t (lower bound) or +inf when missed.
-// min/max slab form (a NaN from 0 * inf leaves the bound; inverted boxes pass — both only widen).
-__device__ __forceinline__ float node4_child(const DNode4F& nd, int k, const RayF& r, v3 o, v3 inv, float tminf,
-                                             float tmaxf, double t_min, double t_max) {
-  if (r.fast) {
-    const float x0 = fmaf(nd.lo[0][k], r.ix, -r.oix), x1 = fmaf(nd.hi[0][k], r.ix, -r.oix);
-    const float y0 = fmaf(nd.lo[1][k], r.iy, -r.oiy), y1 = fmaf(nd.hi[1][k], r.iy, -r.oiy);
-    const float z0 = fmaf(nd.lo[2][k], r.iz, -r.oiz), z1 = fmaf(nd.hi[2][k], r.iz, -r.oiz);
-    const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tminf));
-    const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tmaxf));
-    return tn <= tf ? tn : __builtin_inff();
-  }
-  // far origins: the same inflated box in f64 (exact arithmetic on a superset box)
-  double tn = t_min, tf = t_max;
+// Conservative tests of the four children of a 4-wide node: per child the entry t (a lower bound)
+// or +inf when missed; min/max slab form (a NaN from 0 * inf leaves the bound; inverted boxes pass —
+// both only widen).  The node's six box rows are loaded up front (six 16-B reads), the f32 slab
+// arithmetic runs two children per packed instruction (v_pk_fma_f32), and only a ray with a far
+// origin (max|o| > origin_limit: rare, divergent) re-evaluates the same boxes in f64 (exact arithmetic
+// on a superset box).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 f2(float a, float b) { return f32x2{a, b}; }
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+__device__ __forceinline__ void node4_keys(const DNode4F& nd, const RayF& r, v3 o, v3 inv, float tminf, float tmaxf,
+                                           double t_min, double t_max, float& k0, float& k1, float& k2, float& k3) {
+  const float4 lx = *reinterpret_cast<const float4*>(nd.lo[0]);
+  const float4 ly = *reinterpret_cast<const float4*>(nd.lo[1]);
+  const float4 lz = *reinterpret_cast<const float4*>(nd.lo[2]);
+  const float4 hx = *reinterpret_cast<const float4*>(nd.hi[0]);
+  const float4 hy = *reinterpret_cast<const float4*>(nd.hi[1]);
+  const float4 hz = *reinterpret_cast<const float4*>(nd.hi[2]);
+  const f32x2 ix = f2(r.ix, r.ix), iy = f2(r.iy, r.iy), iz = f2(r.iz, r.iz);
+  const f32x2 nx = f2(-r.oix, -r.oix), ny = f2(-r.oiy, -r.oiy), nz = f2(-r.oiz, -r.oiz);
+  float key[4];
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    const double iv = comp(inv, a), oa = comp(o, a);
-    const double t0 = ((double)nd.lo[a][k] - oa) * iv, t1 = ((double)nd.hi[a][k] - oa) * iv;
-    tn = fmax(tn, fmin(t0, t1));
-    tf = fmin(tf, fmax(t0, t1));
+  for (int h = 0; h < 2; ++h) {  // children (2h, 2h + 1)
+    const f32x2 x0 = pk_fma(h ? f2(lx.z, lx.w) : f2(lx.x, lx.y), ix, nx);
+    const f32x2 x1 = pk_fma(h ? f2(hx.z, hx.w) : f2(hx.x, hx.y), ix, nx);
+    const f32x2 y0 = pk_fma(h ? f2(ly.z, ly.w) : f2(ly.x, ly.y), iy, ny);
+    const f32x2 y1 = pk_fma(h ? f2(hy.z, hy.w) : f2(hy.x, hy.y), iy, ny);
+    const f32x2 z0 = pk_fma(h ? f2(lz.z, lz.w) : f2(lz.x, lz.y), iz, nz);
+    const f32x2 z1 = pk_fma(h ? f2(hz.z, hz.w) : f2(hz.x, hz.y), iz, nz);
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const float tn = fmaxf(fmaxf(fminf(x0[e], x1[e]), fminf(y0[e], y1[e])), fmaxf(fminf(z0[e], z1[e]), tminf));
+      const float tf = fminf(fminf(fmaxf(x0[e], x1[e]), fmaxf(y0[e], y1[e])), fminf(fmaxf(z0[e], z1[e]), tmaxf));
+      key[2 * h + e] = tn <= tf ? tn : __builtin_inff();
+    }
   }
-  return tn <= tf ? __double2float_rd(tn) : __builtin_inff();
+  if (!r.fast) {  // far origins: the same inflated boxes in f64 (exact arithmetic on a superset box)
+    const float lo[3][4] = {{lx.x, lx.y, lx.z, lx.w}, {ly.x, ly.y, ly.z, ly.w}, {lz.x, lz.y, lz.z, lz.w}};
+    const float hi[3][4] = {{hx.x, hx.y, hx.z, hx.w}, {hy.x, hy.y, hy.z, hy.w}, {hz.x, hz.y, hz.z, hz.w}};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      double tn = t_min, tf = t_max;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const double iv = comp(inv, a), oa = comp(o, a);
+        const double t0 = ((double)lo[a][k] - oa) * iv, t1 = ((double)hi[a][k] - oa) * iv;
+        tn = fmax(tn, fmin(t0, t1));
+        tf = fmin(tf, fmax(t0, t1));
+      }
+      key[k] = tn <= tf ? __double2float_rd(tn) : __builtin_inff();
+    }
+  }
+  k0 = key[0];
+  k1 = key[1];
+  k2 = key[2];
+  k3 = key[3];
 }
 
 // The reference's bounding_box() of a leaf object, exactly: sphere c -+ r with the signed radius
@@ -591,12 +625,11 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
                                       double& t_best, int& best, int& face_best, int& sp, int* stk_node,
                                       float* stk_t, unsigned& visits, unsigned& ptests) {
   const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
-  int c0 = nd.child[0], c1 = nd.child[1], c2 = nd.child[2], c3 = nd.child[3];
+  const int4 ch = *reinterpret_cast<const int4*>(nd.child);
+  int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
   const float tminf = __double2float_rd(t_min), tmaxf = __double2float_ru(t_best);
-  float k0 = node4_child(nd, 0, rf, o, inv, tminf, tmaxf, t_min, t_best);
-  float k1 = node4_child(nd, 1, rf, o, inv, tminf, tmaxf, t_min, t_best);
-  float k2 = node4_child(nd, 2, rf, o, inv, tminf, tmaxf, t_min, t_best);
-  float k3 = node4_child(nd, 3, rf, o, inv, tminf, tmaxf, t_min, t_best);
+  float k0, k1, k2, k3;
+  node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
   const float kInf = __builtin_inff();
   visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
   const unsigned lm = (k0 < kInf && c0 < 0 ? 1u : 0u) | (k1 < kInf && c1 < 0 ? 2u : 0u) |
@@ -857,6 +890,81 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
   return need ? 0.5 * (1.0 + sin(sc * p.z + turb)) : 0.0;
 }
 
+// One Philox block of a lane's stream: draws 2c (c0, c1) and 2c + 1 (c2, c3) of (seed, pixel, sample).
+__device__ __forceinline__ void philox_block(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t c, uint64_t& even,
+                                             uint64_t& odd) {
+  uint32_t c0 = c, c1 = sample, c2 = pixel, c3 = 0u;
+  philox10(c0, c1, c2, c3, (uint32_t)seed, (uint32_t)(seed >> 32));
+  even = (uint64_t)c0 | ((uint64_t)c1 << 32);
+  odd = (uint64_t)c2 | ((uint64_t)c3 << 32);
+}
+__device__ __forceinline__ double unit_draw(uint64_t v) { return (double)(v >> 11) * (1.0 / 9007199254740992.0); }
+
+// core/math.rs:32-45 random_in_unit_sphere for every lane with `need`, by the whole wave.  Each such
+// lane first makes its own attempt (the serial loop's first iteration, 52 % accepted).  The lanes it
+// rejected are then served together: all 64 lanes evaluate one later attempt each — attempt i of the
+// pending lane of rank q sits on lane q + i·n (n pending lanes) — and every owner takes its first
+// accepted attempt.  An attempt is a pure function of (seed, pixel, sample, draw index) (Philox is
+// counter-based): attempt at draw t uses draws t, t+1, t+2 = halves of blocks t/2 and t/2 + 1.  So
+// the point, the draw counter after it (t + 3) and the cached odd half (block t/2 + 1's) are exactly
+// the serial loop's, while a wave runs ~3 rounds instead of the ~6 iterations its unluckiest lane
+// needs.  Must be called in wave-uniform control flow (it shuffles).
+__device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, bool need) {
+  v3 p = V(0.0, 0.0, 0.0);
+  bool pending = false;
+  if (need) {
+    const double x = random_real(r, seed, -1.0, 1.0);
+    const double y = random_real(r, seed, -1.0, 1.0);
+    const double z = random_real(r, seed, -1.0, 1.0);
+    p = V(x, y, z);
+    pending = !(len2(p) <= 1.0);
+  }
+  unsigned long long mask = __ballot(pending);
+  if (mask == 0ull) return p;
+  const int lane = __lane_id();
+  while (mask != 0ull) {
+    const int n = __popcll(mask);
+    const int rank = __popcll(mask & lanes_below());  // meaningful for pending lanes
+    const int q = lane % n, i = lane / n;
+    const int owner = select_lane(mask, q);
+    const uint32_t t = (uint32_t)__shfl((int)r.draw, owner) + 3u * (uint32_t)i;
+    const uint32_t pix = (uint32_t)__shfl((int)r.pixel, owner), smp = (uint32_t)__shfl((int)r.sample, owner);
+    uint64_t a0, a1, b0, b1;
+    philox_block(seed, pix, smp, t >> 1, a0, a1);
+    philox_block(seed, pix, smp, (t >> 1) + 1u, b0, b1);
+    const bool odd = (t & 1u) != 0u;
+    const double x = -1.0 + (1.0 - -1.0) * unit_draw(odd ? a1 : a0);  // random_real(-1, 1), same ops
+    const double y = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b0 : a1);
+    const double z = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b1 : b0);
+    const unsigned long long acc = __ballot(len2(V(x, y, z)) <= 1.0);
+    // owners' first accepted attempt, level by level (wave-uniform masks of n bits)
+    const unsigned long long owners = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
+    unsigned long long found = 0ull;
+    int src = -1, lvl = 0;
+    for (int base = 0; base < 64 && found != owners; base += n, ++lvl) {
+      const unsigned long long bits = (acc >> base) & owners;
+      if (pending && ((bits & ~found) >> rank) & 1ull) src = lvl;
+      found |= bits;
+    }
+    const int sl = src >= 0 ? src * n + rank : 0;
+    const double sx = __shfl(x, sl), sy = __shfl(y, sl), sz = __shfl(z, sl);
+    const uint32_t s2 = (uint32_t)__shfl((int)(uint32_t)b1, sl), s3 = (uint32_t)__shfl((int)(uint32_t)(b1 >> 32), sl);
+    if (pending) {
+      if (src >= 0) {
+        p = V(sx, sy, sz);
+        r.draw += 3u * (uint32_t)src + 3u;
+        r.c2 = s2;
+        r.c3 = s3;
+        pending = false;
+      } else {
+        r.draw += 3u * (uint32_t)((64 - rank + n - 1) / n);  // this round's attempts of this owner
+      }
+    }
+    mask = __ballot(pending);
+  }
+  return p;
+}
+
 // checker.rs:28-30
 __device__ __noinline__ double checker_sines(double s, double x, double y, double z) {
   return sin(s * x) * sin(s * y) * sin(s * z);
@@ -1039,9 +1147,10 @@ __device__ __forceinline__ bool shade(const DScene& S, const DPerlin* lds_perlin
   return true;
 }
 
-// shade() with the texture leaf already resolved and its marble value (if any) computed by the wave
-// (marble_coop); same steps otherwise.
-__device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, Rng& rng,
+// shade() with the texture leaf already resolved, its marble value (if any) and the scatter's
+// random_in_unit_sphere point `r` (lambertian / metal / fairy light) computed by the wave
+// (marble_coop, random_in_unit_sphere_coop); same steps otherwise.
+__device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, v3 r, Rng& rng,
                                           uint64_t seed, v3& o, v3& d, const Hit& h, int prim, int face, v3& att,
                                           v3& em) {
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
@@ -1060,7 +1169,6 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
     return true;  // attenuation = Color::ones()
   }
-  v3 r = random_in_unit_sphere(rng, seed);
   if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
     v3 reflected = reflect(unit(d), h.normal);
     o = h.point;

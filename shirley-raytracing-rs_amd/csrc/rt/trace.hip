@@ -14,7 +14,8 @@
 //     tests, nearest-first traversal, per-lane stack in LDS laid out [depth][lane] (conflict-free
 //     at any depth); for scenes that fit, the nodes, primitives and Perlin tables live in LDS too
 //     (one 768-thread block per CU);
-//   * Perlin marble octaves of a segment are dealt across the whole wave (marble_coop);
+//   * Perlin marble octaves and rejection-sampling attempts of a segment are dealt across the whole
+//     wave (marble_coop, random_in_unit_sphere_coop);
 //   * per-unit partial sums go to HBM once; a reduce kernel sums chunks in order (deterministic).
 #include "rt_device.h"
 
@@ -158,7 +159,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     const unsigned long long ph_before = ph_lane_steps;
 #endif
     // (a) closest hit, hit record, and the texture leaf of a diffuse / emitting material
-    bool hit = false, need_pn = false;
+    bool hit = false, need_pn = false, need_r = false;
     int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0;
     double t_best = __builtin_inf(), psc = 0.0;
     Hit h;
@@ -186,6 +187,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
         prim_record<false>(pr, face, o, d, t_best, h);
         mat = pr.material;
         const int mk = S.mats[mat].kind;
+        need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT;
         if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT) {
           leaf = resolve_texture(S, S.mats[mat].tex, h.point);
           const DTex& tx = S.texs[leaf];
@@ -200,12 +202,14 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     // (b) Perlin marble values for the lanes that need one, by the whole wave (wave-uniform)
     const double pn = lds_perlin ? marble_coop((LdsPerlin*)lds_perlin, need_pn, ptab, psc, h.point)
                                  : marble_coop(S.perlin, need_pn, ptab, psc, h.point);
+    // (b') the scatter's random_in_unit_sphere for the lanes whose material draws one, by the wave
+    const v3 rs = random_in_unit_sphere_coop(rng, seed, need_r);
     // (c) emitted + scatter (render.rs:31-45) or the sky
     if (active) {
       bool alive;
       if (hit) {
         const DMat m = S.mats[mat];
-        alive = shade_pre(S, m, leaf, pn, rng, seed, o, d, h, prim, face, att, em);
+        alive = shade_pre(S, m, leaf, pn, rs, rng, seed, o, d, h, prim, face, att, em);
       } else {
         em = em + hmul(att, sky(S, d));
         alive = false;
