@@ -561,47 +561,52 @@ __device__ __forceinline__ void leaf_box(const DPrim& pr, double* b) {
 // The hit leaf children of a 4-wide node against the running closest, each exactly as
 // bbox_tree.rs:60-71 does: f64 hit2 on the object's own bounding box, then the object.  Sphere
 // leaves first in their own loop (sphere.rs:28-46 only), then rect / box leaves, each in child order:
-// a wave runs the rect / box code only when one of its lanes holds such a leaf.
+// a wave runs the rect / box code only when one of its lanes holds such a leaf.  A hit also lowers
+// tmaxf (the f32 upper bound of t_best the node tests use).
+__device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
+  const int lo = (k & 1) ? c1 : c0, hi = (k & 1) ? c3 : c2;
+  return (k & 2) ? hi : lo;
+}
+// f32 upper bound of a t: rounded up, and finite so that a +inf key (a miss) never passes `k <= tmaxf`
+__device__ __forceinline__ float tmax_f32(double t) { return fminf(__double2float_ru(t), 3.402823466e38f); }
+
 template <int MODE>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
                                             RaySigns ns, double a, double t_min, unsigned lm, int c0, int c1,
-                                            int c2, int c3, double& t_best, int& best, int& face_best,
-                                            unsigned& ptests) {
-  unsigned sph = 0, gen = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int c = k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3;
-    if (lm & (1u << k)) {
-      if ((~c) & kLeafGeneric) gen |= 1u << k;
-      else sph |= 1u << k;
-    }
-  }
+                                            int c2, int c3, double& t_best, float& tmaxf, int& best,
+                                            int& face_best, unsigned& ptests) {
+  // non-sphere leaves carry kLeafGeneric in ~child (bit 29 of ~c); lm holds leaf children only
+  const unsigned gm = (((unsigned)~c0 >> 29) & 1u) | ((((unsigned)~c1 >> 29) & 1u) << 1) |
+                      ((((unsigned)~c2 >> 29) & 1u) << 2) | ((((unsigned)~c3 >> 29) & 1u) << 3);
+  unsigned sph = lm & ~gm, gen = lm & gm;
+  bool hit = false;
 #pragma unroll 1
   while (sph) {
     const int k = __builtin_ctz(sph);
     sph &= sph - 1;
-    const int leaf = ~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
+    const int leaf = ~child_at(k, c0, c1, c2, c3);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     const double r = pr.p[3];
     const double b[6] = {pr.p[0] - r, pr.p[1] - r, pr.p[2] - r, pr.p[0] + r, pr.p[1] + r, pr.p[2] + r};
     double te, t;
     if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
     ++ptests;
-    if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; }
+    if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
 #pragma unroll 1
   while (gen) {
     const int k = __builtin_ctz(gen);
     gen &= gen - 1;
-    const int leaf = (~(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3)) & (kLeafGeneric - 1);
+    const int leaf = (~child_at(k, c0, c1, c2, c3)) & (kLeafGeneric - 1);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double b[6], te, t;
     leaf_box(pr, b);
     if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
     int f = -1;
     ++ptests;
-    if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; }
+    if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
+  if (hit) tmaxf = tmax_f32(t_best);
 }
 
 // compare-exchange of (key, node) pairs: ascending key
@@ -618,23 +623,28 @@ __device__ __forceinline__ void cas(float& ka, int& na, float& kb, int& nb) {
 // One node visit: conservative f32 tests of the four child boxes; hit leaf children tested exactly
 // at once (they can shrink t_best); hit internal children visited nearest-first (4-entry sorting
 // network on the f32 entry t), the others pushed with that lower bound and skipped on pop when
-// beyond the closest hit.  Returns the next node, or -1 when the traversal is complete.
+// beyond the closest hit.  The cull compares the f32 entry with tmaxf >= t_best: it may keep a
+// subtree the exact comparison would drop (entry in (t_best, tmaxf]), never the reverse, and extra
+// visits cannot change the closest hit (leaf tests are exact).  `sp` is the stack offset in
+// elements (depth x STRIDE).  Returns the next node, or -1 when the traversal is complete.
 template <int STRIDE, int MODE>
 __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                       v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
-                                      double& t_best, int& best, int& face_best, int& sp, int* stk_node,
-                                      float* stk_t, unsigned& visits, unsigned& ptests) {
+                                      double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
+                                      int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
   const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
   const int4 ch = *reinterpret_cast<const int4*>(nd.child);
   int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-  const float tminf = __double2float_rd(t_min), tmaxf = __double2float_ru(t_best);
+  const float tminf = __double2float_rd(t_min);
   float k0, k1, k2, k3;
   node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
   const float kInf = __builtin_inff();
   visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
   const unsigned lm = (k0 < kInf && c0 < 0 ? 1u : 0u) | (k1 < kInf && c1 < 0 ? 2u : 0u) |
                       (k2 < kInf && c2 < 0 ? 4u : 0u) | (k3 < kInf && c3 < 0 ? 8u : 0u);
-  if (lm) leaf_tests4<MODE>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, best, face_best, ptests);
+  if (lm)
+    leaf_tests4<MODE>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, tmaxf, best, face_best,
+                      ptests);
   // internal children nearest-first: leaves, empty slots and misses sort last (key inf)
   if (c0 < 0 || c0 == kEmptyChild) k0 = kInf;
   if (c1 < 0 || c1 == kEmptyChild) k1 = kInf;
@@ -645,15 +655,15 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
   cas(k0, c0, k2, c2);
   cas(k1, c1, k3, c3);
   cas(k1, c1, k2, c2);
-  const double tb = t_best;
-  if (k3 < kInf && (double)k3 <= tb) { stk_node[sp * STRIDE] = c3; stk_t[sp * STRIDE] = k3; ++sp; }
-  if (k2 < kInf && (double)k2 <= tb) { stk_node[sp * STRIDE] = c2; stk_t[sp * STRIDE] = k2; ++sp; }
-  if (k1 < kInf && (double)k1 <= tb) { stk_node[sp * STRIDE] = c1; stk_t[sp * STRIDE] = k1; ++sp; }
-  if (k0 < kInf && (double)k0 <= tb) return c0;
+  const float tb = tmaxf;  // finite: inf keys fail every test below
+  if (k3 <= tb) { stk_node[sp] = c3; stk_t[sp] = k3; sp += STRIDE; }
+  if (k2 <= tb) { stk_node[sp] = c2; stk_t[sp] = k2; sp += STRIDE; }
+  if (k1 <= tb) { stk_node[sp] = c1; stk_t[sp] = k1; sp += STRIDE; }
+  if (k0 <= tb) return c0;
   while (sp > 0) {
-    --sp;
+    sp -= STRIDE;
     // a pushed subtree whose (lower-bound) entry lies beyond the current closest hit cannot hold it
-    if ((double)stk_t[sp * STRIDE] <= tb) return stk_node[sp * STRIDE];
+    if (stk_t[sp] <= tb) return stk_node[sp];
   }
   return -1;
 }
@@ -674,6 +684,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
   const RaySigns ns = ray_signs(inv);
   const RayF rf = ray_f(S, o, inv);
   const double a = len2(d);
+  float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;
   int node = 0;  // top node: child[0] = root
@@ -683,8 +694,8 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
 #ifdef RT_PHASE_TIMING
     ++g_trav_lane_steps;
 #endif
-    node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, best, face_best,
-                                sp, stk_node, stk_t, visits, ptests);
+    node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, tmaxf, best,
+                                face_best, sp, stk_node, stk_t, visits, ptests);
   }
   return best;
 }
@@ -693,6 +704,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
 struct Trav4 {
   v3 inv;
   double a, t_best;
+  float tmaxf;
   int best, face, node, sp, steps;
   RaySigns ns;
   RayF rf;
@@ -704,6 +716,7 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
   T.rf = ray_f(S, o, T.inv);
   T.a = len2(d);
   T.t_best = t_max;
+  T.tmaxf = tmax_f32(t_max);
   T.best = -1;
   T.face = -1;
   T.node = 0;
@@ -718,7 +731,7 @@ __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_n
                                            unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
   T.node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
-                                T.best, T.face, T.sp, stk_node, stk_t, visits, ptests);
+                                T.tmaxf, T.best, T.face, T.sp, stk_node, stk_t, visits, ptests);
   return T.node < 0;
 }
 
