@@ -21,6 +21,9 @@ namespace rt {
 size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads);
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
+#ifdef RT_PHASE_TIMING
+void phase_counters_dump();
+#endif
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
                          int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
 hipError_t launch_tonemap(const double* accum, int width, int height, double inv, uint8_t* rgb8, hipStream_t stream);
@@ -344,8 +347,9 @@ void flatten4(const BuiltTree& t, const rt_scene_desc* d, double delta, std::vec
     const BuildNode& bn = t.nodes[it.built];
     set_child_box(out[it.parent], it.slot, &bn.box, delta);
     if (bn.leaf >= 0) {
-      const bool sphere = d->objects[bn.leaf].geometry == RT_GEOM_SPHERE;
-      out[it.parent].child[it.slot] = ~(bn.leaf | (sphere ? 0 : kLeafGeneric));
+      const int32_t g = d->objects[bn.leaf].geometry;
+      const int32_t flags = g == RT_GEOM_SPHERE ? 0 : (g == RT_GEOM_RECT_BOX ? kLeafGeneric | kLeafBox : kLeafGeneric);
+      out[it.parent].child[it.slot] = ~(bn.leaf | flags);
       continue;
     }
     const int32_t idx = (int32_t)out.size();
@@ -744,7 +748,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const int32_t placement = builder & placement_mask;
   builder &= ~placement_mask;
   if (builder != RT_BVH_REFERENCE && builder != RT_BVH_SAH) return fail(c, RT_E_INVALID, "bad bvh builder %d", builder);
-  if (d->n_objects >= kLeafGeneric) return fail(c, RT_E_UNSUPPORTED, "too many objects (%d)", d->n_objects);
+  if (d->n_objects > kLeafPrimMask) return fail(c, RT_E_UNSUPPORTED, "too many objects (%d)", d->n_objects);
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->have_scene = false;
@@ -1041,6 +1045,7 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
     }
     fprintf(stderr, "[phase] traversal lane steps %.4g, wave steps %.4g, SIMD utilisation %.3f\n", lane, wave,
             lane / (64.0 * wave));
+    phase_counters_dump();
   }
 #endif
   float a = 0.f, b = 0.f;

@@ -448,6 +448,18 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
 #ifdef RT_PHASE_TIMING
 // per-lane step counter of the instrumented build (a register of the calling kernel)
 #define g_trav_lane_steps trav_lane_steps_ref
+// event counters of the instrumented build: slot 2i += active lanes, slot 2i + 1 += 1 (per wave)
+static __device__ unsigned long long g_phase_ctr[32];
+__device__ __forceinline__ void ph_count(int i) {
+  const unsigned long long act = __ballot(1);
+  if ((int)__lane_id() == __builtin_ctzll(act)) {
+    atomicAdd(&g_phase_ctr[2 * i], (unsigned long long)__popcll(act));
+    atomicAdd(&g_phase_ctr[2 * i + 1], 1ull);
+  }
+}
+#define PH_COUNT(i) ph_count(i)
+#else
+#define PH_COUNT(i)
 #endif
 template <int MODE>
 __device__ __forceinline__ const DNode4F& fetch_node4(const DScene& S, const DNode4F* lds_nodes, int idx) {
@@ -559,29 +571,35 @@ __device__ __forceinline__ void leaf_box(const DPrim& pr, double* b) {
 }
 
 // The hit leaf children of a 4-wide node against the running closest, each exactly as
-// bbox_tree.rs:60-71 does: f64 hit2 on the object's own bounding box, then the object.  Sphere
-// leaves first in their own loop (sphere.rs:28-46 only), then rect / box leaves, each in child order:
-// a wave runs the rect / box code only when one of its lanes holds such a leaf.  A hit also lowers
-// tmaxf (the f32 upper bound of t_best the node tests use).
+// bbox_tree.rs:60-71 does: f64 hit2 on the object's own bounding box, then the object.  One loop per
+// leaf kind — spheres (sphere.rs:28-46), rects (rect.rs:54-65), boxes (rect.rs:132-156) — each in
+// child order, so a wave runs a kind's code only while one of its lanes holds a leaf of that kind.
+// (Which of several leaves with exactly equal t wins is the one tie the reference's own tree order
+// decides; see DESIGN.md.)  A hit also lowers tmaxf (the f32 bound of t_best the node tests use).
 __device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
   const int lo = (k & 1) ? c1 : c0, hi = (k & 1) ? c3 : c2;
   return (k & 2) ? hi : lo;
 }
 // f32 upper bound of a t: rounded up, and finite so that a +inf key (a miss) never passes `k <= tmaxf`
 __device__ __forceinline__ float tmax_f32(double t) { return fminf(__double2float_ru(t), 3.402823466e38f); }
+// 4-bit mask of the children whose ~child has bit `b` set
+__device__ __forceinline__ unsigned flag_mask(int c0, int c1, int c2, int c3, int b) {
+  return (((unsigned)~c0 >> b) & 1u) | ((((unsigned)~c1 >> b) & 1u) << 1) | ((((unsigned)~c2 >> b) & 1u) << 2) |
+         ((((unsigned)~c3 >> b) & 1u) << 3);
+}
 
 template <int MODE>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
                                             RaySigns ns, double a, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, double& t_best, float& tmaxf, int& best,
                                             int& face_best, unsigned& ptests) {
-  // non-sphere leaves carry kLeafGeneric in ~child (bit 29 of ~c); lm holds leaf children only
-  const unsigned gm = (((unsigned)~c0 >> 29) & 1u) | ((((unsigned)~c1 >> 29) & 1u) << 1) |
-                      ((((unsigned)~c2 >> 29) & 1u) << 2) | ((((unsigned)~c3 >> 29) & 1u) << 3);
-  unsigned sph = lm & ~gm, gen = lm & gm;
+  // lm holds leaf children only
+  const unsigned gm = flag_mask(c0, c1, c2, c3, 29), bm = flag_mask(c0, c1, c2, c3, 28);
+  unsigned sph = lm & ~gm, rect = lm & gm & ~bm, box = lm & bm;
   bool hit = false;
 #pragma unroll 1
   while (sph) {
+    PH_COUNT(2);
     const int k = __builtin_ctz(sph);
     sph &= sph - 1;
     const int leaf = ~child_at(k, c0, c1, c2, c3);
@@ -590,21 +608,41 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     const double b[6] = {pr.p[0] - r, pr.p[1] - r, pr.p[2] - r, pr.p[0] + r, pr.p[1] + r, pr.p[2] + r};
     double te, t;
     if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
+    PH_COUNT(3);
     ++ptests;
     if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
 #pragma unroll 1
-  while (gen) {
-    const int k = __builtin_ctz(gen);
-    gen &= gen - 1;
-    const int leaf = (~child_at(k, c0, c1, c2, c3)) & (kLeafGeneric - 1);
+  while (rect) {
+    PH_COUNT(4);
+    const int k = __builtin_ctz(rect);
+    rect &= rect - 1;
+    const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double b[6], te, t;
     leaf_box(pr, b);
     if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
-    int f = -1;
     ++ptests;
-    if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
+    bool h;
+    switch (pr.kind) {
+      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t); break;
+      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t); break;
+      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t);
+    }
+    if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
+  }
+#pragma unroll 1
+  while (box) {
+    PH_COUNT(7);
+    const int k = __builtin_ctz(box);
+    box &= box - 1;
+    const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
+    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
+    double te, t;
+    if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
+    ++ptests;
+    const int f = box_t(pr.p, o, d, t_min, t_best, t);
+    if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
   if (hit) tmaxf = tmax_f32(t_best);
 }
@@ -632,6 +670,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
                                       v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
                                       int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
+  PH_COUNT(0);
   const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
   const int4 ch = *reinterpret_cast<const int4*>(nd.child);
   int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
@@ -642,6 +681,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
   visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
   const unsigned lm = (k0 < kInf && c0 < 0 ? 1u : 0u) | (k1 < kInf && c1 < 0 ? 2u : 0u) |
                       (k2 < kInf && c2 < 0 ? 4u : 0u) | (k3 < kInf && c3 < 0 ? 8u : 0u);
+  if (lm) PH_COUNT(1);
   if (lm)
     leaf_tests4<MODE>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, tmaxf, best, face_best,
                       ptests);
@@ -661,6 +701,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
   if (k1 <= tb) { stk_node[sp] = c1; stk_t[sp] = k1; sp += STRIDE; }
   if (k0 <= tb) return c0;
   while (sp > 0) {
+    PH_COUNT(5);
     sp -= STRIDE;
     // a pushed subtree whose (lower-bound) entry lies beyond the current closest hit cannot hold it
     if (stk_t[sp] <= tb) return stk_node[sp];
@@ -877,6 +918,7 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
   const int total = 7 * k;
   double accum = 0.0;
   for (int base = 0; base < total; base += 64) {
+    PH_COUNT(8);
     const int item = base + lane;
     const bool valid = item < total;
     const int oct = valid ? item / k : 0;
@@ -936,6 +978,7 @@ __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, 
   if (mask == 0ull) return p;
   const int lane = __lane_id();
   while (mask != 0ull) {
+    PH_COUNT(9);
     const int n = __popcll(mask);
     const int rank = __popcll(mask & lanes_below());  // meaningful for pending lanes
     const int q = lane % n, i = lane / n;

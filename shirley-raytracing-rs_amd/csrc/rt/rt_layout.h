@@ -38,9 +38,12 @@ static_assert(sizeof(DNode) == 112, "DNode layout");
 // are its children's, so whenever the reference passes a leaf's box it passes every enclosing box
 // too — internal tests never decide which primitives are tested; leaf tests do, and those run
 // exactly (f64 hit2 on the leaf's own bounding box, recomputed from the primitive).
-// child >= 0: node index; child < 0: leaf ~(prim | kLeafGeneric when not a sphere), so traversal can
-// test sphere leaves in a tight loop and rects / boxes in a second one; kEmptyChild: none.
+// child >= 0: node index; child < 0: leaf ~(prim | kind flags): kLeafGeneric when not a sphere, plus
+// kLeafBox for a RectBox, so traversal tests sphere, rect and box leaves in three tight loops (a wave
+// runs each leaf kind's code once per round, not the union of all kinds); kEmptyChild: none.
 constexpr int32_t kLeafGeneric = 1 << 29;
+constexpr int32_t kLeafBox = 1 << 28;
+constexpr int32_t kLeafPrimMask = kLeafBox - 1;  // primitive index bits
 struct alignas(16) DNode4F {
   float lo[3][4];  // lo[axis][child]
   float hi[3][4];

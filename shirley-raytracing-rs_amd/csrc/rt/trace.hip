@@ -170,6 +170,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
 #ifdef RT_PHASE_TIMING
     unsigned long long ph2 = ph1;
 #endif
+    PH_COUNT(6);
     if (active) {
       ++n_seg;
 #ifdef RT_PHASE_TIMING
@@ -470,6 +471,22 @@ hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, 
                      ty0, tile_rank, tile_world, width, row0, row1, packed, out);
   return hipGetLastError();
 }
+
+#ifdef RT_PHASE_TIMING
+// instrumented build: print and clear the event counters (slot 2i: lane events, 2i + 1: wave events)
+void phase_counters_dump() {
+  unsigned long long h[32];
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_ctr), sizeof h) != hipSuccess) return;
+  static const char* names[] = {"visit", "visit_with_leaves", "sphere_iter", "sphere_slab_pass", "rect_iter",
+                                "pop_iter", "segment_iter", "box_iter", "marble_round", "sphere_coop_round"};
+  for (int i = 0; i < 10; ++i)
+    if (h[2 * i + 1])
+      fprintf(stderr, "[phase-ev] %-18s lanes %.4g waves %.4g lanes/wave %.2f\n", names[i], (double)h[2 * i],
+              (double)h[2 * i + 1], (double)h[2 * i] / (double)h[2 * i + 1]);
+  unsigned long long z[32] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_ctr), z, sizeof z);
+}
+#endif
 
 hipError_t launch_tonemap(const double* accum, int width, int height, double inv, uint8_t* rgb8, hipStream_t stream) {
   const long long n = (long long)width * height * 3;
