@@ -827,6 +827,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.nodes4 = static_cast<const DNode4F*>(c->nodes4.p);
   S.n_nodes4 = (int32_t)nodes4.size();
   S.stack_depth4 = stack4;
+  S.root4 = (nodes4[0].child[0] >= 0 && nodes4[0].child[0] != kEmptyChild) ? nodes4[0].child[0] : 0;
   S.origin_limit = infl.origin_limit;
   S.prims = static_cast<const DPrim*>(c->prims.p);
   S.mats = static_cast<const DMat*>(c->mats.p);

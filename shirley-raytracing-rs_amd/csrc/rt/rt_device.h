@@ -728,7 +728,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
   float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;
-  int node = 0;  // top node: child[0] = root
+  int node = S.root4;
   // a tree traversal visits every node at most once: more steps than nodes can only be a defect,
   // and ends the loop instead of hanging the wave
   for (int steps = 0; steps < S.n_nodes4 && node >= 0; ++steps) {
@@ -760,7 +760,7 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
   T.tmaxf = tmax_f32(t_max);
   T.best = -1;
   T.face = -1;
-  T.node = 0;
+  T.node = S.root4;
   T.sp = 0;
   T.steps = 0;
 }

@@ -112,6 +112,8 @@ struct DScene {
   int32_t n_lds_perlin;    // 0, or n_perlin when the megakernel block also keeps the Perlin tables in LDS
   float origin_limit;      // rays with max|o| <= origin_limit take the f32 node test (its error bound
                            // assumes it); others evaluate the same inflated boxes in f64
+  int32_t root4;           // first 4-wide node a traversal visits: the root when it is internal (its
+                           // own box test only culls, so it is skipped), else the top node 0
   int32_t sky;
   double sky_color[3];
 };
