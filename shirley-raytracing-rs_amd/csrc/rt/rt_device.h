@@ -29,6 +29,40 @@ __device__ __forceinline__ v3 unit(v3 a) {
   double n = len(a);
   return V(a.x / n, a.y / n, a.z / n);
 }
+// Exact division by a shared reciprocal.  The compiler lowers a / b (binary64, correctly rounded)
+// to: b' = div_scale(b), r0 = rcp(b'), two Newton steps r = fma(r, fma(-b', r, 1), r), a' =
+// div_scale(a), q0 = a' r, e = fma(-b', q0, a'), q = div_fmas(e, r, q0), div_fixup(q).  With |a| and
+// |b| in [2^-300, 2^300] both div_scale steps are the identity (no exponent gap >= 768, no denormal
+// or tiny operand or quotient), div_fmas is a plain fma and div_fixup only re-applies the quotient's
+// sign — so a / b = fma(fma(-b, a r, a), r, a r) with r from b alone, and divisions by one b can share
+// r (the rcp and the Newton steps) at a mul and two fmas each.  Bit-identity is checked by
+// tools/divcheck.hip (tests/test_gpu_divcheck.py).
+struct Recip {
+  double b, r;
+};
+__device__ __forceinline__ Recip recip(double b) {
+  double r = __builtin_amdgcn_rcp(b);  // v_rcp_f64
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  r = __builtin_fma(r, __builtin_fma(-b, r, 1.0), r);
+  return Recip{b, r};
+}
+// a / R.b for |a|, |R.b| in [2^-300, 2^300] (the caller checks)
+__device__ __forceinline__ double div_recip(double a, const Recip& R) {
+  const double q0 = a * R.r;
+  return __builtin_fma(__builtin_fma(-R.b, q0, a), R.r, q0);
+}
+// unit() with the three divisions by |a| sharing one reciprocal when every operand is in range
+// (|components| >= 2^-300 and |a| <= 2^300; |components| <= |a| up to rounding); else unit()'s own
+// divisions.  Same bits as unit() either way.
+__device__ __forceinline__ v3 unit_fast(v3 a) {
+  const double n = len(a);
+  const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
+  if (mn >= 0x1p-300 && n <= 0x1p300) {
+    const Recip R = recip(n);
+    return V(div_recip(a.x, R), div_recip(a.y, R), div_recip(a.z, R));
+  }
+  return V(a.x / n, a.y / n, a.z / n);
+}
 __device__ __forceinline__ double comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 // vec3.rs:129-132
 __device__ __forceinline__ bool near_zero(v3 a) {
@@ -1147,6 +1181,15 @@ __device__ __noinline__ double reflectance(double cosine, double ref_idx) {
 }
 
 // skybox/mod.rs:5-25
+// skybox/mod.rs:18-25 given un = unit(d)
+__device__ __forceinline__ v3 sky_unit(const DScene& S, v3 un) {
+  if (S.sky == RT_SKY_ABOVE) {
+    double t = 0.5 * (un.y + 1.0);
+    return scale(V(1.0, 1.0, 1.0), 1.0 - t) + scale(V(0.5, 0.7, 1.0), t);
+  }
+  if (S.sky == RT_SKY_FLAT) return V(S.sky_color[0], S.sky_color[1], S.sky_color[2]);
+  return V(0.0, 0.0, 0.0);
+}
 __device__ __forceinline__ v3 sky(const DScene& S, v3 d) {
   if (S.sky == RT_SKY_ABOVE) {
     v3 un = unit(d);
@@ -1203,12 +1246,14 @@ __device__ __forceinline__ bool shade(const DScene& S, const DPerlin* lds_perlin
   return true;
 }
 
-// shade() with the texture leaf already resolved, its marble value (if any) and the scatter's
-// random_in_unit_sphere point `r` (lambertian / metal / fairy light) computed by the wave
-// (marble_coop, random_in_unit_sphere_coop); same steps otherwise.
-__device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, v3 r, Rng& rng,
-                                          uint64_t seed, v3& o, v3& d, const Hit& h, int prim, int face, v3& att,
-                                          v3& em) {
+// shade() with the wave-level parts done beforehand: the texture leaf resolved, its marble value
+// (if any) and the scatter's random_in_unit_sphere point `r` (lambertian / metal / fairy light)
+// computed by the wave (marble_coop, random_in_unit_sphere_coop), and `un` = the one unit vector the
+// material needs — unit(r) for lambertian / fairy light, unit(d) for dielectric / metal — computed
+// for all lanes at once instead of once per material branch.  Same steps otherwise.
+__device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, v3 r, v3 un,
+                                          Rng& rng, uint64_t seed, v3& o, v3& d, const Hit& h, int prim,
+                                          int face, v3& att, v3& em) {
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
     v3 e = leaf_texture_value(S, leaf, pn, prim, face, h);
     em = em + hmul(att, e);
@@ -1216,7 +1261,7 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
   }
   if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
     double ratio = h.front_face ? (1.0 / m.param) : m.param;
-    v3 ud = unit(d);
+    const v3 ud = un;
     double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
     double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
     bool refl = ratio * sin_theta > 1.0;
@@ -1226,7 +1271,7 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     return true;  // attenuation = Color::ones()
   }
   if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
-    v3 reflected = reflect(unit(d), h.normal);
+    v3 reflected = reflect(un, h.normal);
     o = h.point;
     d = reflected + scale(r, m.param);
     att = hmul(att, V(m.albedo[0], m.albedo[1], m.albedo[2]));
@@ -1239,7 +1284,7 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     em = em + hmul(att, scale(a, s / len(d)));
     a = unit(a);
   }
-  v3 sc = h.normal + unit(r);
+  v3 sc = h.normal + un;
   if (near_zero(sc)) sc = h.normal;
   o = h.point;
   d = sc;

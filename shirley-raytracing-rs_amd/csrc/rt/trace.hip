@@ -160,7 +160,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
 #endif
     // (a) closest hit, hit record, and the texture leaf of a diffuse / emitting material
     bool hit = false, need_pn = false, need_r = false;
-    int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0;
+    int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0, mk = -1;
     double t_best = __builtin_inf(), psc = 0.0;
     Hit h;
     h.point = V(0.0, 0.0, 0.0);
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
         const DPrim pr = S.prims[prim];
         prim_record<false>(pr, face, o, d, t_best, h);
         mat = pr.material;
-        const int mk = S.mats[mat].kind;
+        mk = S.mats[mat].kind;
         need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT;
         if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT) {
           leaf = resolve_texture(S, S.mats[mat].tex, h.point);
@@ -205,14 +205,17 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
                                  : marble_coop(S.perlin, need_pn, ptab, psc, h.point);
     // (b') the scatter's random_in_unit_sphere for the lanes whose material draws one, by the wave
     const v3 rs = random_in_unit_sphere_coop(rng, seed, need_r);
+    // (b'') the one normalisation a lane's shading needs, for all lanes at once: unit(r) for a
+    // lambertian / fairy light hit, unit(d) for dielectric, metal and the sky (idle lanes: a dummy)
+    const v3 un = unit_fast(!active ? V(1.0, 1.0, 1.0) : (need_r && mk != RT_MAT_METAL) ? rs : d);
     // (c) emitted + scatter (render.rs:31-45) or the sky
     if (active) {
       bool alive;
       if (hit) {
         const DMat m = S.mats[mat];
-        alive = shade_pre(S, m, leaf, pn, rs, rng, seed, o, d, h, prim, face, att, em);
+        alive = shade_pre(S, m, leaf, pn, rs, un, rng, seed, o, d, h, prim, face, att, em);
       } else {
-        em = em + hmul(att, sky(S, d));
+        em = em + hmul(att, sky_unit(S, un));
         alive = false;
       }
       if (alive) alive = --depth_left > 0;
