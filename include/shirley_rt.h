@@ -161,7 +161,7 @@ typedef struct rt_scene_stats {
 typedef struct rt_counters {
   uint64_t samples;     /* paths started = pixels x spp */
   uint64_t segments;    /* ray_color loop iterations that traced a ray (hit + miss) */
-  uint64_t node_visits; /* BVH child-box tests */
+  uint64_t node_visits; /* BVH child-box tests (4-wide trees: 4 per node visit) */
   uint64_t prim_tests;  /* primitive intersection calls */
   double kernel_ms;     /* device time of the trace (all trace kernels of the frame, HIP events) */
   double reduce_ms;     /* device time of the partial-sum reduce kernel */

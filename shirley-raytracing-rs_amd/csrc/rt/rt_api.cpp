@@ -828,6 +828,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.n_nodes4 = (int32_t)nodes4.size();
   S.stack_depth4 = stack4;
   S.root4 = (nodes4[0].child[0] >= 0 && nodes4[0].child[0] != kEmptyChild) ? nodes4[0].child[0] : 0;
+  {
+    int kbits = 1;
+    while ((size_t)1 << kbits < nodes4.size()) ++kbits;
+    if (kbits > kMaxKeyBits) return fail(c, RT_E_UNSUPPORTED, "BVH too large (%zu 4-wide nodes)", nodes4.size());
+    S.key_mask = (1u << kbits) - 1u;
+  }
   S.origin_limit = infl.origin_limit;
   S.prims = static_cast<const DPrim*>(c->prims.p);
   S.mats = static_cast<const DMat*>(c->mats.p);
@@ -854,9 +860,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   };
   auto lds_nodes_for = [&](long long stack) { return lds_count(stack, sizeof(DNode), nodes.size()); };
   const long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
-  const long long stack4_bytes = (long long)S.stack_depth4 * kTraceThreads * 8;
+  const long long stack4_bytes = (long long)S.stack_depth4 * kTraceThreads * kStack4EntryBytes;
   const long long wide_bytes =
-      (long long)S.stack_depth4 * kTraceThreadsWide * 8 + (long long)nodes4.size() * sizeof(DNode4F);
+      (long long)S.stack_depth4 * kTraceThreadsWide * kStack4EntryBytes + (long long)nodes4.size() * sizeof(DNode4F);
   if (stack_bytes > kLdsBytes || stack4_bytes > kLdsBytes)
     return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
   const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS);

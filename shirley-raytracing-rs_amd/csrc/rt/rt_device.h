@@ -681,75 +681,73 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
   if (hit) tmaxf = tmax_f32(t_best);
 }
 
-// compare-exchange of (key, node) pairs: ascending key
-__device__ __forceinline__ void cas(float& ka, int& na, float& kb, int& nb) {
-  const bool sw = kb < ka;
-  const float k = sw ? kb : ka;
-  const int n = sw ? nb : na;
-  kb = sw ? ka : kb;
-  nb = sw ? na : nb;
-  ka = k;
-  na = n;
-}
-
 // One node visit: conservative f32 tests of the four child boxes; hit leaf children tested exactly
-// at once (they can shrink t_best); hit internal children visited nearest-first (4-entry sorting
-// network on the f32 entry t), the others pushed with that lower bound and skipped on pop when
-// beyond the closest hit.  The cull compares the f32 entry with tmaxf >= t_best: it may keep a
-// subtree the exact comparison would drop (entry in (t_best, tmaxf]), never the reverse, and extra
-// visits cannot change the closest hit (leaf tests are exact).  `sp` is the stack offset in
+// at once (they can shrink t_best); hit internal children visited nearest-first, the others pushed
+// and skipped on pop when beyond the closest hit.
+// A child is one 32-bit word: its f32 entry t (> 0, so its bits order like the value) with the low K
+// bits (S.key_mask) replaced by the node index — a lower bound of the entry, so culling with it stays
+// conservative; misses, leaves and empty slots are ~0u.  Sorting is then 5 min/max pairs, a stack
+// entry is one word, and the cull `entry <= tmaxf` is one unsigned compare against bits(tmaxf) | mask.
+// tmaxf >= t_best: the cull may keep a subtree the exact comparison would drop, never the reverse, and
+// extra visits cannot change the closest hit (leaf tests are exact).  `sp` is the stack offset in
 // elements (depth x STRIDE).  Returns the next node, or -1 when the traversal is complete.
+__device__ __forceinline__ void cas_u(unsigned& a, unsigned& b) {
+  const unsigned lo = min(a, b), hi = max(a, b);
+  a = lo;
+  b = hi;
+}
 template <int STRIDE, int MODE>
 __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                       v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
-                                      int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
+                                      unsigned* stk, unsigned& visits, unsigned& ptests) {
   PH_COUNT(0);
   const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
   const int4 ch = *reinterpret_cast<const int4*>(nd.child);
-  int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-  const float tminf = __double2float_rd(t_min);
+  const int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+  const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
   float k0, k1, k2, k3;
   node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
   const float kInf = __builtin_inff();
-  visits += (c0 != kEmptyChild) + (c1 != kEmptyChild) + (c2 != kEmptyChild) + (c3 != kEmptyChild);
+  visits += 4;
   const unsigned lm = (k0 < kInf && c0 < 0 ? 1u : 0u) | (k1 < kInf && c1 < 0 ? 2u : 0u) |
                       (k2 < kInf && c2 < 0 ? 4u : 0u) | (k3 < kInf && c3 < 0 ? 8u : 0u);
   if (lm) PH_COUNT(1);
   if (lm)
     leaf_tests4<MODE>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, tmaxf, best, face_best,
                       ptests);
-  // internal children nearest-first: leaves, empty slots and misses sort last (key inf)
-  if (c0 < 0 || c0 == kEmptyChild) k0 = kInf;
-  if (c1 < 0 || c1 == kEmptyChild) k1 = kInf;
-  if (c2 < 0 || c2 == kEmptyChild) k2 = kInf;
-  if (c3 < 0 || c3 == kEmptyChild) k3 = kInf;
-  cas(k0, c0, k1, c1);
-  cas(k2, c2, k3, c3);
-  cas(k0, c0, k2, c2);
-  cas(k1, c1, k3, c3);
-  cas(k1, c1, k2, c2);
-  const float tb = tmaxf;  // finite: inf keys fail every test below
-  if (k3 <= tb) { stk_node[sp] = c3; stk_t[sp] = k3; sp += STRIDE; }
-  if (k2 <= tb) { stk_node[sp] = c2; stk_t[sp] = k2; sp += STRIDE; }
-  if (k1 <= tb) { stk_node[sp] = c1; stk_t[sp] = k1; sp += STRIDE; }
-  if (k0 <= tb) return c0;
+  // internal children (0 <= c < kEmptyChild) as packed words; a miss (k = inf) packs above any bound
+  const unsigned km = S.key_mask;
+  unsigned p0 = (unsigned)c0 < (unsigned)kEmptyChild ? ((__float_as_uint(k0) & ~km) | (unsigned)c0) : ~0u;
+  unsigned p1 = (unsigned)c1 < (unsigned)kEmptyChild ? ((__float_as_uint(k1) & ~km) | (unsigned)c1) : ~0u;
+  unsigned p2 = (unsigned)c2 < (unsigned)kEmptyChild ? ((__float_as_uint(k2) & ~km) | (unsigned)c2) : ~0u;
+  unsigned p3 = (unsigned)c3 < (unsigned)kEmptyChild ? ((__float_as_uint(k3) & ~km) | (unsigned)c3) : ~0u;
+  cas_u(p0, p1);
+  cas_u(p2, p3);
+  cas_u(p0, p2);
+  cas_u(p1, p3);
+  cas_u(p1, p2);
+  const unsigned lim = __float_as_uint(tmaxf) | km;  // tmaxf finite: inf entries fail
+  if (p3 <= lim) { stk[sp] = p3; sp += STRIDE; }
+  if (p2 <= lim) { stk[sp] = p2; sp += STRIDE; }
+  if (p1 <= lim) { stk[sp] = p1; sp += STRIDE; }
+  if (p0 <= lim) return (int)(p0 & km);
   while (sp > 0) {
     PH_COUNT(5);
     sp -= STRIDE;
     // a pushed subtree whose (lower-bound) entry lies beyond the current closest hit cannot hold it
-    if (stk_t[sp] <= tb) return stk_node[sp];
+    const unsigned e = stk[sp];
+    if (e <= lim) return (int)(e & km);
   }
   return -1;
 }
 
-// Whole closest-hit query over the 4-wide tree.  The conservative internal tests and the exact
-// leaf tests make the set of primitives that can win the reference's (see DNode4F); the closest hit
-// is the reference's up to exact ties in t.
+// Whole closest-hit query over the 4-wide tree (t_min > 0).  The conservative internal tests and the
+// exact leaf tests make the set of primitives that can win the reference's (see DNode4F); the closest
+// hit is the reference's up to exact ties in t.
 template <int STRIDE, int MODE>
 __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
-                                         double t_min,
-                                         double& t_best, int& face_best, int* stk_node, float* stk_t,
+                                         double t_min, double& t_best, int& face_best, unsigned* stk,
                                          unsigned& visits, unsigned& ptests
 #ifdef RT_PHASE_TIMING
                                          , unsigned long long& trav_lane_steps_ref
@@ -770,7 +768,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
     ++g_trav_lane_steps;
 #endif
     node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, tmaxf, best,
-                                face_best, sp, stk_node, stk_t, visits, ptests);
+                                face_best, sp, stk, visits, ptests);
   }
   return best;
 }
@@ -802,11 +800,11 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
 // Returns true when the traversal is complete (T.best / T.t_best / T.face hold the closest hit).
 template <int STRIDE, int MODE>
 __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o,
-                                           v3 d, double t_min, Trav4& T, int* stk_node, float* stk_t,
-                                           unsigned& visits, unsigned& ptests) {
+                                           v3 d, double t_min, Trav4& T, unsigned* stk, unsigned& visits,
+                                           unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
   T.node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
-                                T.tmaxf, T.best, T.face, T.sp, stk_node, stk_t, visits, ptests);
+                                T.tmaxf, T.best, T.face, T.sp, stk, visits, ptests);
   return T.node < 0;
 }
 

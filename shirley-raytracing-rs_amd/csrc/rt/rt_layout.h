@@ -44,6 +44,8 @@ static_assert(sizeof(DNode) == 112, "DNode layout");
 constexpr int32_t kLeafGeneric = 1 << 29;
 constexpr int32_t kLeafBox = 1 << 28;
 constexpr int32_t kLeafPrimMask = kLeafBox - 1;  // primitive index bits
+constexpr int kMaxKeyBits = 20;      // node-index bits of a traversal entry (so <= 2^20 4-wide nodes)
+constexpr int kStack4EntryBytes = 4; // one packed (entry t | node) word per 4-wide stack entry
 struct alignas(16) DNode4F {
   float lo[3][4];  // lo[axis][child]
   float hi[3][4];
@@ -114,6 +116,8 @@ struct DScene {
                            // assumes it); others evaluate the same inflated boxes in f64
   int32_t root4;           // first 4-wide node a traversal visits: the root when it is internal (its
                            // own box test only culls, so it is skipped), else the top node 0
+  uint32_t key_mask;       // 2^K - 1 >= n_nodes4 - 1: a 4-wide traversal entry is one 32-bit word,
+                           // the f32 entry t with its low K bits replaced by the node index
   int32_t sky;
   double sky_color[3];
 };

@@ -49,8 +49,7 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
                             (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) +
                                                      (size_t)P.scene.n_lds_perlin * sizeof(DPerlin)
                                                : 0);
-  int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
-  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
+  unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;  // [stack_depth4][THREADS] packed entries
   stage_nodes4<MODE>(P.scene, lds_nodes, lds_prims);
 
   const DScene& S = P.scene;
@@ -174,13 +173,12 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     if (active) {
       ++n_seg;
 #ifdef RT_PHASE_TIMING
-      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits,
-                                      ptests, ph_lane_steps);
+      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, visits, ptests,
+                                      ph_lane_steps);
       ph2 = clock64();
       ph_trav += ph2 - ph1;
 #else
-      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk_node, stk_t, visits,
-                                      ptests);
+      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, visits, ptests);
 #endif
       if (prim >= 0) {
         hit = true;
@@ -378,11 +376,11 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
-// megakernel block LDS: [n_lds_nodes4 x DNode4F][n_lds_prims x DPrim][stack_depth4 x threads int]
-// [stack_depth4 x threads float]
+// megakernel block LDS: [n_lds_nodes4 x DNode4F][n_lds_prims x DPrim][n_lds_perlin x DPerlin]
+// [stack_depth4 x threads packed entries]
 size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads) {
   return (size_t)n_lds_nodes4 * sizeof(DNode4F) + (size_t)n_lds_prims * sizeof(DPrim) +
-         (size_t)n_lds_perlin * sizeof(DPerlin) + (size_t)stack_depth4 * threads * 8;
+         (size_t)n_lds_perlin * sizeof(DPerlin) + (size_t)stack_depth4 * threads * kStack4EntryBytes;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 

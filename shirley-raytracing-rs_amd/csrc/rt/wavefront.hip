@@ -144,8 +144,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
   unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
                             (size_t)P.scene.n_lds_prims * sizeof(DPrim) + (size_t)P.scene.n_lds_perlin * sizeof(DPerlin);
-  int* stk_node = reinterpret_cast<int*>(stk_base) + tid;
-  float* stk_t = reinterpret_cast<float*>(stk_base + (size_t)P.scene.stack_depth4 * THREADS * 4) + tid;
+  unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;  // [stack_depth4][THREADS] packed entries
   stage_nodes4<kSceneLds>(P.scene, lds_nodes, lds_prims);
   const DScene& S = P.scene;
   const WfState& st = P.st;
@@ -207,8 +206,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
       continue;
     }
     // C. one node visit for every lane holding a ray
-    if (active && trav4_step<THREADS, kSceneLds>(S, lds_nodes, lds_prims, o, d, 0.001, T, stk_node, stk_t, visits,
-                                                 ptests)) {
+    if (active && trav4_step<THREADS, kSceneLds>(S, lds_nodes, lds_prims, o, d, 0.001, T, stk, visits, ptests)) {
       st.ht[slot] = T.t_best;
       st.hprim[slot] = T.best;
       st.hface[slot] = T.face;
@@ -571,7 +569,7 @@ static int wf_mode(const DScene& S) {
 
 size_t wf_extend4_lds(const DScene& S) {
   return (size_t)S.n_lds_nodes4 * sizeof(DNode4F) + (size_t)S.n_lds_prims * sizeof(DPrim) +
-         (size_t)S.n_lds_perlin * sizeof(DPerlin) + (size_t)S.stack_depth4 * kTraceThreadsWide * 8;
+         (size_t)S.n_lds_perlin * sizeof(DPerlin) + (size_t)S.stack_depth4 * kTraceThreadsWide * kStack4EntryBytes;
 }
 
 // The 4-wide, scene-in-LDS extend kernel for scenes where the megakernel runs wide (`S` = that scene).
