@@ -179,6 +179,28 @@ __device__ __forceinline__ bool slab_s(const double* b, v3 o, v3 inv, RaySigns n
   return !(t_max <= t_min);
 }
 
+// slab_s on a sphere's bounding box (c - r, c + r) (sphere.rs:54-60), with the near / far plane of
+// each axis formed as c + rn and c - rn, rn = (1/d < 0) ? r : -r: the same two sums slab_s selects
+// between (x - y == x + (-y) in IEEE arithmetic), for one sign flip instead of four selects per axis.
+__device__ __forceinline__ double sel_neg(bool neg, double r) {
+  // r with its sign bit flipped unless neg (the low word is shared)
+  const int hi = __double2hiint(r);
+  return __hiloint2double(neg ? hi : (hi ^ (int)0x80000000), __double2loint(r));
+}
+__device__ __forceinline__ bool slab_sphere(const double* p, v3 o, v3 inv, RaySigns ns, double t_min, double t_max) {
+  const double r = p[3];
+  double rn = sel_neg(ns.x, r);
+  t_min = fmax(((p[0] + rn) - o.x) * inv.x, t_min);
+  t_max = fmin(((p[0] - rn) - o.x) * inv.x, t_max);
+  rn = sel_neg(ns.y, r);
+  t_min = fmax(((p[1] + rn) - o.y) * inv.y, t_min);
+  t_max = fmin(((p[1] - rn) - o.y) * inv.y, t_max);
+  rn = sel_neg(ns.z, r);
+  t_min = fmax(((p[2] + rn) - o.z) * inv.z, t_min);
+  t_max = fmin(((p[2] - rn) - o.z) * inv.z, t_max);
+  return !(t_max <= t_min);
+}
+
 // sphere.rs:28-46 (t only)
 __device__ __forceinline__ bool sphere_t(const double* p, v3 o, v3 d, double a, double t_min, double t_max,
                                          double& t) {
@@ -497,7 +519,10 @@ __device__ __forceinline__ void ph_count(int i) {
 #endif
 template <int MODE>
 __device__ __forceinline__ const DNode4F& fetch_node4(const DScene& S, const DNode4F* lds_nodes, int idx) {
-  if (MODE == kNodesLds || MODE == kSceneLds) return lds_nodes[idx];
+  // LDS byte offset with a full-rate 24-bit multiply (an LDS node index is < 2^24)
+  if (MODE == kNodesLds || MODE == kSceneLds)
+    return *reinterpret_cast<const DNode4F*>(reinterpret_cast<const char*>(lds_nodes) +
+                                             __umul24((unsigned)idx, (unsigned)sizeof(DNode4F)));
   if (MODE == kNodesGlobal) return S.nodes4[idx];
   return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : S.nodes4[idx];
 }
@@ -638,10 +663,8 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     sph &= sph - 1;
     const int leaf = ~child_at(k, c0, c1, c2, c3);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-    const double r = pr.p[3];
-    const double b[6] = {pr.p[0] - r, pr.p[1] - r, pr.p[2] - r, pr.p[0] + r, pr.p[1] + r, pr.p[2] + r};
-    double te, t;
-    if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
+    if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
+    double t;
     PH_COUNT(3);
     ++ptests;
     if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
