@@ -95,6 +95,9 @@ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
+    // the round keys are recomputed here (two s_add per round) rather than hoisted out of every loop
+    // as 20 live SGPRs, which the kernel would spill to VGPR lanes and reload with v_readlane
+    asm volatile("" : "+s"(k0), "+s"(k1));
     // one 32x32->64 product per multiplier (v_mad_u64_u32) instead of separate mul_lo / mul_hi
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);

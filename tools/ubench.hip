@@ -1,0 +1,92 @@
+// Issue cost of the VALU instructions the trace kernel leans on (gfx950), measured with s_memtime:
+// one wave per SIMD (4 waves per CU, all CUs), 8 independent chains per lane, N iterations.
+// Prints shader cycles per wave-instruction.  Diagnostic only.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHAINS 8
+template <int OP>
+__global__ __launch_bounds__(768) void kern(int n, unsigned long long* out, unsigned* sink) {
+  unsigned a[CHAINS];
+  double f[CHAINS];
+  unsigned long long w[CHAINS];
+  for (int i = 0; i < CHAINS; ++i) {
+    a[i] = threadIdx.x * 7919u + i;
+    f[i] = 1.0 + 1e-3 * (threadIdx.x + i);
+    w[i] = a[i];
+  }
+  unsigned k = 0xD2511F53u;
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int it = 0; it < n; ++it) {
+#pragma unroll
+    for (int i = 0; i < CHAINS; ++i) {
+      if (OP == 0) asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(w[i]) : "v"(a[i]), "s"(k) : "vcc");
+      if (OP == 1) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a[i]) : "s"(k));
+      if (OP == 2) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(a[i]) : "s"(k));
+      if (OP == 3) asm volatile("v_mul_u32_u24 %0, %0, %1" : "+v"(a[i]) : "s"(k));
+      if (OP == 4) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "s"(k));
+      if (OP == 5) asm volatile("v_fma_f64 %0, %0, %0, 1.0" : "+v"(f[i]));
+      if (OP == 6) asm volatile("v_add_f64 %0, %0, 1.0" : "+v"(f[i]));
+      if (OP == 7) asm volatile("v_rcp_f64 %0, %0" : "+v"(f[i]));
+      if (OP == 8) asm volatile("v_sqrt_f64 %0, %0" : "+v"(f[i]));
+      if (OP == 9) asm volatile("v_fma_f32 %0, %0, %0, 1.0" : "+v"(a[i]));
+      if (OP == 10) asm volatile("v_pk_fma_f32 %0, %0, %0, %0" : "+v"(w[i]));
+      if (OP == 11) asm volatile("v_div_scale_f64 %0, vcc, %0, %0, 1.0" : "+v"(f[i]) : : "vcc");
+      if (OP == 12) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]));
+      if (OP == 13) asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(f[i]) : "v"(a[i]));
+      if (OP == 14) asm volatile("v_ldexp_f64 %0, %0, 1" : "+v"(f[i]));
+      if (OP == 15) asm volatile("v_readlane_b32 %0, %1, 5" : "=s"(k) : "v"(a[i]));
+      if (OP == 16) asm volatile("v_min_f64 %0, %0, %0" : "+v"(f[i]));
+      if (OP == 17) asm volatile("v_cmp_lt_f64 vcc, %0, %1" : : "v"(f[i]), "v"(f[(i + 1) % CHAINS]) : "vcc");
+      if (OP == 18) asm volatile("ds_bpermute_b32 %0, %1, %0\n s_waitcnt lgkmcnt(0)" : "+v"(a[i]) : "v"(a[(i + 3) % CHAINS]));
+    }
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  unsigned s = 0;
+  for (int i = 0; i < CHAINS; ++i) s ^= a[i] ^ (unsigned)w[i] ^ (unsigned)(w[i] >> 32) ^ (unsigned)__double_as_longlong(f[i]);
+  if (s == 0x12345678u) sink[0] = s;
+  if (threadIdx.x % 64 == 0) out[blockIdx.x * 12 + threadIdx.x / 64] = t1 - t0;
+}
+
+static int g_threads = 256;
+template <int OP>
+double run(int n, int blocks, unsigned long long* d, unsigned* sink) {
+  hipLaunchKernelGGL(kern<OP>, dim3(blocks), dim3(g_threads), 0, 0, n, d, sink);
+  hipLaunchKernelGGL(kern<OP>, dim3(blocks), dim3(g_threads), 0, 0, n, d, sink);
+  (void)hipDeviceSynchronize();
+  static unsigned long long h[4096 * 3];
+  const int waves = blocks * g_threads / 64;
+  (void)hipMemcpy(h, d, blocks * 12 * 8, hipMemcpyDeviceToHost);
+  double s = 0;
+  int cnt = 0;
+  for (int b = 0; b < blocks; ++b)
+    for (int w = 0; w < g_threads / 64; ++w) { s += (double)h[b * 12 + w]; ++cnt; }
+  (void)waves;
+  // per-SIMD issue cost: per-wave time / (waves per SIMD)
+  return s / cnt / ((double)n * CHAINS) / (g_threads / 256.0);
+}
+
+int main(int argc, char** argv) {
+  const int n = 4096, blocks = 256;
+  g_threads = argc > 1 ? atoi(argv[1]) : 256;
+  unsigned long long* d;
+  unsigned* sink;
+  (void)hipMalloc(&d, 4096 * 12 * 8);
+  (void)hipMalloc(&sink, 4);
+  const char* names[] = {"v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_u32_u24", "v_xor_b32",
+                         "v_fma_f64", "v_add_f64", "v_rcp_f64", "v_sqrt_f64", "v_fma_f32", "v_pk_fma_f32",
+                         "v_div_scale_f64", "v_cndmask_b32", "v_cvt_f64_u32", "v_ldexp_f64", "v_readlane_b32",
+                         "v_min_f64", "v_cmp_lt_f64", "ds_bpermute+wait"};
+  double c[19];
+  c[0] = run<0>(n, blocks, d, sink); c[1] = run<1>(n, blocks, d, sink); c[2] = run<2>(n, blocks, d, sink);
+  c[3] = run<3>(n, blocks, d, sink); c[4] = run<4>(n, blocks, d, sink); c[5] = run<5>(n, blocks, d, sink);
+  c[6] = run<6>(n, blocks, d, sink); c[7] = run<7>(n, blocks, d, sink); c[8] = run<8>(n, blocks, d, sink);
+  c[9] = run<9>(n, blocks, d, sink); c[10] = run<10>(n, blocks, d, sink); c[11] = run<11>(n, blocks, d, sink);
+  c[12] = run<12>(n, blocks, d, sink); c[13] = run<13>(n, blocks, d, sink); c[14] = run<14>(n, blocks, d, sink);
+  c[15] = run<15>(n, blocks, d, sink); c[16] = run<16>(n, blocks, d, sink); c[17] = run<17>(n, blocks, d, sink);
+  c[18] = run<18>(n, blocks, d, sink);
+  printf("threads/block %d (%d waves per SIMD): SIMD cycles per wave-instruction\n", g_threads, g_threads / 256);
+  for (int i = 0; i < 19; ++i) printf("%-18s %6.2f\n", names[i], c[i]);
+  return 0;
+}
