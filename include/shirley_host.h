@@ -34,7 +34,8 @@ int32_t sh_scene_len(const sh_scene* s);
 int sh_scene_to_json(const sh_scene* s, int32_t pretty, char* buf, size_t cap, size_t* needed);
 int sh_scene_from_json(const char* json, sh_scene** out); /* render saved (scenes.rs:128-134) */
 /* scenes.rs entry points by name: random, random-night, demo, perlin, earth, box-light, cornell,
- * spheres[:side] (gen_spheres stand-in for BASELINE config 5) */
+ * spheres[:side] (gen_spheres), final[:n_ground[:n_cluster]] (book-2 final_scene, BASELINE config 5;
+ * uses the book-2 extensions the reference lacks) */
 int sh_scene_builtin(const char* name, uint64_t seed, sh_scene** out);
 
 /* SceneBuilder::finalize (scene/mod.rs:111-137): textures loaded + deduplicated, Perlin tables from
@@ -54,6 +55,7 @@ typedef struct sh_camera_spec {
   double look_from[3], look_at[3], up[3];
   int32_t override_focus; /* pos.focus_length = focus_length after look_at (scenes.rs:209,229) */
   double focus_length;
+  double time0, time1;    /* shutter (book-2 extension, absent from the reference) */
 } sh_camera_spec;
 int sh_camera_build(const sh_camera_spec* spec, rt_camera* out);
 /* scenes.rs:214-231 default_camera(CameraSettings) ; argparse.rs:125-170 defaults: 640, 20, 1.0, 0.001, std3x2 */

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -38,9 +38,15 @@ typedef enum rt_status {
 } rt_status;
 
 /* geometry/object.rs:9-16  GeometricObject */
-enum { RT_GEOM_SPHERE = 0, RT_GEOM_RECT_XY = 1, RT_GEOM_RECT_YZ = 2, RT_GEOM_RECT_XZ = 3, RT_GEOM_RECT_BOX = 4 };
+enum { RT_GEOM_SPHERE = 0, RT_GEOM_RECT_XY = 1, RT_GEOM_RECT_YZ = 2, RT_GEOM_RECT_XZ = 3, RT_GEOM_RECT_BOX = 4,
+       /* book-2 ("The Next Week") extension, absent from the reference:
+        * a sphere whose centre moves linearly from p[0..2] at q[3] to q[0..2] at q[4] */
+       RT_GEOM_MOVING_SPHERE = 5 };
 /* material/material_type.rs:20-27  MaterialType */
-enum { RT_MAT_METAL = 0, RT_MAT_DIELECTRIC = 1, RT_MAT_LAMBERTIAN = 2, RT_MAT_DIFFUSE_LIGHT = 3, RT_MAT_FAIRY_LIGHT = 4 };
+enum { RT_MAT_METAL = 0, RT_MAT_DIELECTRIC = 1, RT_MAT_LAMBERTIAN = 2, RT_MAT_DIFFUSE_LIGHT = 3, RT_MAT_FAIRY_LIGHT = 4,
+       /* book-2 extension (absent from the reference): the phase function of a ConstantMedium —
+        * scatters to random_in_unit_sphere() with the texture's albedo */
+       RT_MAT_ISOTROPIC = 5 };
 /* material/texture/loader.rs:17-28  TextureLoader (after load: Solid / Checker / Noise / Image) */
 enum { RT_TEX_SOLID = 0, RT_TEX_CHECKER = 1, RT_TEX_PERLIN = 2, RT_TEX_IMAGE = 3 };
 /* skybox/mod.rs:11-16  SkyBox */
@@ -64,14 +70,24 @@ enum {
   RT_ENGINE_TIMING = 0x10   /* flag: time every kernel launch with HIP events (rt_counters *_ms) */
 };
 
-/* One scene object = SceneLoadObject{geometry, material} (scene/mod.rs:23-27). */
+/* One scene object = SceneLoadObject{geometry, material} (scene/mod.rs:23-27).
+ * The fields after p[] are book-2 ("The Next Week") extensions that the reference does not have
+ * (SURVEY.md §0.1 config 5); all zero = a reference object.  Their semantics are DESIGN.md §10's
+ * (parity unpinned: no reference implementation exists). */
 typedef struct rt_object {
   int32_t geometry; /* RT_GEOM_* */
   int32_t material; /* index into rt_scene_desc.materials */
   /* Sphere  (geometry/sphere.rs:11-15): cx cy cz radius (radius may be negative: sphere.rs:48,54-60)
    * Rect    (geometry/rect.rs:45-52):   d1_min d1_max d2_min d2_max offset
-   * RectBox (geometry/rect.rs:102-130): min.x min.y min.z max.x max.y max.z (sides derived as RectBox::new) */
+   * RectBox (geometry/rect.rs:102-130): min.x min.y min.z max.x max.y max.z (sides derived as RectBox::new)
+   * MovingSphere: center0 xyz, radius */
   double p[6];
+  int32_t medium;     /* 1: a ConstantMedium whose boundary is this geometry (material: RT_MAT_ISOTROPIC) */
+  int32_t transform;  /* 1: instance transform, world = Translate(offset) . RotateY(rotate_y_deg) . object */
+  double q[5];        /* MovingSphere: center1 xyz, time0, time1 */
+  double density;     /* ConstantMedium density (neg_inv_density = -1/density) */
+  double rotate_y_deg;
+  double offset[3];
 } rt_object;
 
 typedef struct rt_material {
@@ -136,6 +152,9 @@ typedef struct rt_camera {
   double origin[3];
   double w[3], u[3], v[3];
   double focus_length;
+  /* shutter interval (book-2 extension, absent from the reference): a path's ray time is
+   * time0 + (time1 - time0) * U, U from its own counter-RNG stream; only moving spheres read it */
+  double time0, time1;
 } rt_camera;
 
 /* Per-call render parameters (RenderSettings, argparse.rs:106-123, plus what the reference lacks). */

@@ -285,6 +285,108 @@ static int rectbox_hit(const double* b, const ray_t* r, double t_min, double t_m
   return have;
 }
 
+/* ------------------------------------------------------------------------------------------ */
+/* book-2 ("The Next Week") extensions — ABSENT from the reference;  */
+/* restated from the book's moving_sphere.h / constant_medium.h / rotate_y / translate / camera */
+/* time, with the deviations DESIGN.md §10 states.  PARITY UNPINNED (no reference to compare). */
+/* ------------------------------------------------------------------------------------------ */
+/* the path key of the ray being traced: side streams for the ray time and a medium's free flight */
+typedef struct hctx_t {
+  uint64_t seed;
+  uint32_t pixel, sample, draw;
+  double time0, time1;
+} hctx_t;
+
+/* side stream: Philox4x32-10 at counter (c0, sample, pixel, stream), stream >= 2^30 */
+static double side_draw(uint64_t seed, uint32_t c0, uint32_t sample, uint32_t pixel, uint32_t stream) {
+  uint32_t ctr[4] = {c0, sample, pixel, stream};
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t o[4];
+  or_philox4x32_10(ctr, key, o);
+  return u64_to_f64((uint64_t)o[0] | ((uint64_t)o[1] << 32));
+}
+#define STREAM_TIME 0x40000000u
+#define STREAM_MEDIUM 0x80000000u
+
+/* camera.h get_ray: time = random_double(time0, time1) (from the path's time stream) */
+static double ray_time(const hctx_t* cx) {
+  return cx->time0 + (cx->time1 - cx->time0) * side_draw(cx->seed, 0u, cx->sample, cx->pixel, STREAM_TIME);
+}
+/* moving_sphere.h center(time) */
+static v3 moving_center(const rt_object* o, double tm) {
+  v3 c0 = V(o->p[0], o->p[1], o->p[2]), c1 = V(o->q[0], o->q[1], o->q[2]);
+  return vadd(c0, vscale(vsub(c1, c0), (tm - o->q[3]) / (o->q[4] - o->q[3])));
+}
+static int object_hit(const rt_object* o, const ray_t* r, double t_min, double t_max, hit_t* out);
+static int sphere_hit(const double* p, const ray_t* r, double t_min, double t_max, hit_t* out);
+/* the object's own shape (reference geometry, or moving_sphere.h hit at the ray's time) */
+static int shape_hit(const rt_object* o, const ray_t* r, double t_min, double t_max, const hctx_t* cx, hit_t* out) {
+  if (o->geometry == RT_GEOM_MOVING_SPHERE) {
+    v3 c = moving_center(o, ray_time(cx));
+    double p[4] = {c.x, c.y, c.z, o->p[3]};
+    return sphere_hit(p, r, t_min, t_max, out);
+  }
+  return object_hit(o, r, t_min, t_max, out);
+}
+/* constant_medium.h hit with the shape as boundary (t2 not clamped to t_max; the scatter t is
+ * compared with t_max instead — equal in exact arithmetic, order-independent); the free-flight
+ * uniform comes from the medium stream keyed by (draw index of the path, object index). */
+static int medium_hit(const rt_object* o, int32_t obj, const ray_t* r, double t_min, double t_max,
+                      const hctx_t* cx, hit_t* out) {
+  hit_t rec1, rec2;
+  if (!shape_hit(o, r, -INFINITY, INFINITY, cx, &rec1)) return 0;
+  if (!shape_hit(o, r, rec1.t + 0.0001, INFINITY, cx, &rec2)) return 0;
+  if (rec1.t < t_min) rec1.t = t_min;
+  if (rec1.t >= rec2.t) return 0;
+  if (rec1.t < 0) rec1.t = 0;
+  double ray_length = vlen(r->d);
+  double distance_inside_boundary = (rec2.t - rec1.t) * ray_length;
+  double neg_inv_density = -1.0 / o->density;
+  double hit_distance = neg_inv_density * log(side_draw(cx->seed, cx->draw, cx->sample, cx->pixel,
+                                                        STREAM_MEDIUM | (uint32_t)obj));
+  if (hit_distance > distance_inside_boundary) return 0;
+  double t = rec1.t + hit_distance / ray_length;
+  if (t > t_max) return 0;
+  out->t = t;
+  out->point = ray_at(r, t);
+  out->normal = V(1.0, 0.0, 0.0); /* arbitrary */
+  out->front_face = 1;            /* also arbitrary */
+  out->u = out->v = 0.0;
+  return 1;
+}
+static void rotate_y_cs(const rt_object* o, double* cs, double* sn) {
+  double radians = o->rotate_y_deg * PI_ / 180.0;
+  *cs = cos(radians);
+  *sn = sin(radians);
+}
+/* translate(rotate_y(inner)): Translate::hit moves the ray by -offset, RotateY::hit rotates it,
+ * the inner hit's point and normal are rotated back and translated (front_face kept). */
+static int ext_object_hit(const rt_object* o, int32_t obj, const ray_t* r, double t_min, double t_max,
+                          const hctx_t* cx, hit_t* out) {
+  if (!o->transform) {
+    if (o->medium) return medium_hit(o, obj, r, t_min, t_max, cx, out);
+    return shape_hit(o, r, t_min, t_max, cx, out);
+  }
+  v3 off = V(o->offset[0], o->offset[1], o->offset[2]);
+  double cs, sn;
+  rotate_y_cs(o, &cs, &sn);
+  ray_t moved = {vsub(r->o, off), r->d};
+  ray_t rot;
+  rot.o = V(cs * moved.o.x - sn * moved.o.z, moved.o.y, sn * moved.o.x + cs * moved.o.z);
+  rot.d = V(cs * moved.d.x - sn * moved.d.z, moved.d.y, sn * moved.d.x + cs * moved.d.z);
+  hit_t h;
+  int ok = o->medium ? medium_hit(o, obj, &rot, t_min, t_max, cx, &h) : shape_hit(o, &rot, t_min, t_max, cx, &h);
+  if (!ok) return 0;
+  v3 p = h.point, n = h.normal;
+  h.point = vadd(V(cs * p.x + sn * p.z, p.y, -sn * p.x + cs * p.z), off);
+  h.normal = V(cs * n.x + sn * n.z, n.y, -sn * n.x + cs * n.z);
+  *out = h;
+  return 1;
+}
+static int is_extended(const rt_object* o) {
+  return o->geometry == RT_GEOM_MOVING_SPHERE || o->medium || o->transform;
+}
+
 /* object.rs:45-58 */
 static int object_hit(const rt_object* o, const ray_t* r, double t_min, double t_max, hit_t* out) {
   switch (o->geometry) {
@@ -301,8 +403,47 @@ static int object_hit(const rt_object* o, const ray_t* r, double t_min, double t
   return 0;
 }
 
-/* sphere.rs:54-60 (signed radius), rect.rs:82-99 (BBOX_WIDTH = 1e-4), rect.rs:158-163 */
+static int reference_bbox(const rt_object* o, aabb_t* out);
+/* bounding boxes of book-2 objects: moving_sphere.h (boxes at time0 and time1, surrounded),
+ * rotate_y.h (8 rotated corners), translate (+offset), constant_medium.h (the boundary's) */
 static int object_bbox(const rt_object* o, aabb_t* out) {
+  aabb_t b;
+  if (o->geometry == RT_GEOM_MOVING_SPHERE) {
+    v3 rr = V(o->p[3], o->p[3], o->p[3]);
+    v3 c0 = moving_center(o, o->q[3]), c1 = moving_center(o, o->q[4]);
+    aabb_t b0 = {vsub(c0, rr), vadd(c0, rr)}, b1 = {vsub(c1, rr), vadd(c1, rr)};
+    b = surrounding(b0, b1);
+  } else if (!reference_bbox(o, &b)) {
+    return 0;
+  }
+  if (o->transform) {
+    double cs, sn;
+    rotate_y_cs(o, &cs, &sn);
+    v3 mn = V(INFINITY, INFINITY, INFINITY), mx = V(-INFINITY, -INFINITY, -INFINITY);
+    for (int i = 0; i < 2; i++)
+      for (int j = 0; j < 2; j++)
+        for (int k = 0; k < 2; k++) {
+          double x = i * b.mx.x + (1 - i) * b.mn.x;
+          double y = j * b.mx.y + (1 - j) * b.mn.y;
+          double z = k * b.mx.z + (1 - k) * b.mn.z;
+          double newx = cs * x + sn * z;
+          double newz = -sn * x + cs * z;
+          v3 tester = V(newx, y, newz);
+          for (int c = 0; c < 3; c++) {
+            vset(&mn, c, fmin(vget(mn, c), vget(tester, c)));
+            vset(&mx, c, fmax(vget(mx, c), vget(tester, c)));
+          }
+        }
+    v3 off = V(o->offset[0], o->offset[1], o->offset[2]);
+    b.mn = vadd(mn, off);
+    b.mx = vadd(mx, off);
+  }
+  *out = b;
+  return 1;
+}
+
+/* sphere.rs:54-60 (signed radius), rect.rs:82-99 (BBOX_WIDTH = 1e-4), rect.rs:158-163 */
+static int reference_bbox(const rt_object* o, aabb_t* out) {
   switch (o->geometry) {
     case RT_GEOM_SPHERE: {
       v3 c = V(o->p[0], o->p[1], o->p[2]);
@@ -557,6 +698,7 @@ void or_tree_node(const or_scene* s, int32_t idx, double bbox[6], int32_t* leaf,
 typedef struct work_t {
   int32_t* stack; /* BboxTreeWorkspace (bbox_tree.rs:38-41) */
   or_counters cnt;
+  hctx_t ctx;     /* key of the path being traced (book-2 extensions only) */
 } work_t;
 
 /* bbox_tree.rs:56-91 hit_workspace */
@@ -579,7 +721,10 @@ static int tree_hit(const or_scene* s, work_t* w, const ray_t* r, double t_min, 
     } else {
       hit_t h;
       w->cnt.prim_tests++;
-      if (object_hit(&s->objects[node->leaf], r, t_min, t_closest, &h)) { closest = h; have = 1; *obj = node->leaf; }
+      const rt_object* o = &s->objects[node->leaf];
+      int ok = is_extended(o) ? ext_object_hit(o, node->leaf, r, t_min, t_closest, &w->ctx, &h)
+                              : object_hit(o, r, t_min, t_closest, &h);
+      if (ok) { closest = h; have = 1; *obj = node->leaf; }
     }
   }
   if (have) *out = closest;
@@ -753,6 +898,12 @@ static int material_scatter(const or_scene* s, const rt_material* m, rng_t* rng,
     }
     case RT_MAT_DIFFUSE_LIGHT: /* lighting.rs:26-28 */
       return 0;
+    case RT_MAT_ISOTROPIC: { /* book-2 isotropic (extension): ray(rec.p, random_in_unit_sphere()) */
+      out->o = h->point;
+      out->d = random_in_unit_sphere(rng);
+      *att = texture_value(s, m->texture, h->u, h->v, h->point);
+      return 1;
+    }
     case RT_MAT_FAIRY_LIGHT: { /* lighting.rs:42-57 */
       v3 sc = vadd(h->normal, random_unit_vector(rng));
       if (near_zero(sc)) sc = h->normal;
@@ -785,6 +936,7 @@ static v3 ray_color(const or_scene* s, work_t* w, rng_t* rng, ray_t ray, int32_t
     hit_t h;
     int32_t obj = -1;
     w->cnt.segments++;
+    w->ctx.draw = rng->draw; /* book-2 media key their free flight by the segment's first draw index */
     if (scene_hit(s, w, &ray, 0.001, INFINITY, &h, &obj)) {
       const rt_material* m = &s->materials[s->objects[obj].material];
       v3 e;
@@ -843,6 +995,11 @@ static v3 sample_color(const or_scene* s, work_t* w, const rt_camera* cam, const
   double jy = (double)py + rng_gen(&rng);
   ray_t r = pixel_ray(cam, &rng, jx, jy);
   w->cnt.samples++;
+  w->ctx.seed = rng.seed;
+  w->ctx.pixel = rng.pixel;
+  w->ctx.sample = rng.sample;
+  w->ctx.time0 = cam->time0;
+  w->ctx.time1 = cam->time1;
   return ray_color(s, w, &rng, r, p->max_depth);
 }
 
@@ -851,6 +1008,7 @@ static int32_t eff_samples(const rt_render_params* p) { return p->samples == 0 ?
 static void work_init(const or_scene* s, work_t* w) {
   w->stack = (int32_t*)malloc(sizeof(int32_t) * (size_t)(s->n_tree + 2));
   memset(&w->cnt, 0, sizeof(w->cnt));
+  memset(&w->ctx, 0, sizeof(w->ctx));
 }
 static void cnt_add(or_counters* a, const or_counters* b) {
   if (!a) return;
@@ -963,22 +1121,30 @@ static void hit_out(const hit_t* h, int32_t obj, or_hit* out) {
 int32_t or_object_hit(const rt_object* obj, const double ray[6], double t_min, double t_max, or_hit* out) {
   ray_t r = ray_from(ray);
   hit_t h;
+  hctx_t cx;
+  memset(&cx, 0, sizeof(cx));
   memset(out, 0, sizeof(*out));
   out->object = -1;
-  if (!object_hit(obj, &r, t_min, t_max, &h)) return 0;
+  if (!(is_extended(obj) ? ext_object_hit(obj, 0, &r, t_min, t_max, &cx, &h) : object_hit(obj, &r, t_min, t_max, &h)))
+    return 0;
   hit_out(&h, -1, out);
   return 1;
 }
-void or_scene_hit(const or_scene* s, const double ray[6], double t_min, double t_max, or_hit* out) {
+void or_scene_hit_at(const or_scene* s, const double ray[6], double t_min, double t_max, uint32_t ray_index,
+                     or_hit* out) {
   ray_t r = ray_from(ray);
   work_t w;
   work_init(s, &w);
+  w.ctx.pixel = ray_index; /* rt_scene_hit's key: (seed 0, pixel = ray index, sample 0, draw 0), time 0 */
   hit_t h;
   int32_t obj = -1;
   memset(out, 0, sizeof(*out));
   out->object = -1;
   if (scene_hit(s, &w, &r, t_min, t_max, &h, &obj)) hit_out(&h, obj, out);
   free(w.stack);
+}
+void or_scene_hit(const or_scene* s, const double ray[6], double t_min, double t_max, or_hit* out) {
+  or_scene_hit_at(s, ray, t_min, t_max, 0u, out);
 }
 void or_texture_value(const or_scene* s, int32_t tex, double u, double v, const double p[3], double out[3]) {
   v3 c = texture_value(s, tex, u, v, V(p[0], p[1], p[2]));

@@ -68,6 +68,9 @@ int32_t or_tree_root(const or_scene* s);
 void or_tree_node(const or_scene* s, int32_t idx, double bbox[6], int32_t* leaf, int32_t* lhs, int32_t* rhs);
 /* WorkspaceScene::hit_workspace (scene/mod.rs:152-164) */
 void or_scene_hit(const or_scene* s, const double ray[6], double t_min, double t_max, or_hit* out);
+/* the same with the key rt_scene_hit gives ray `ray_index` (book-2 media draw from it) */
+void or_scene_hit_at(const or_scene* s, const double ray[6], double t_min, double t_max, uint32_t ray_index,
+                     or_hit* out);
 
 /* texture value (material/texture/{solid,checker,image_texture}.rs, perlin/mod.rs:162-183) */
 void or_texture_value(const or_scene* s, int32_t tex, double u, double v, const double p[3], double out[3]);

@@ -128,6 +128,8 @@ static CameraSpec spec_from(const sh_camera_spec* s) {
   c.up = Vec3(s->up[0], s->up[1], s->up[2]);
   c.override_focus = s->override_focus != 0;
   c.focus_length = s->focus_length;
+  c.time0 = s->time0;
+  c.time1 = s->time1;
   return c;
 }
 
@@ -173,7 +175,8 @@ int sh_scene_camera(const char* name, int32_t width, const char* aspect, double 
   int32_t rn = 3, rd = 2;
   if (aspect && !aspect_ratio_from_name(aspect, &rn, &rd)) return fail(std::string("unknown aspect ratio ") + aspect);
   CameraSpec c = (n.rfind("spheres", 0) == 0) ? spheres_camera_spec(width, rn, rd)
-                                              : default_camera_spec(width, rn, rd, vfov, focal_length, aperture);
+                 : (n.rfind("final", 0) == 0)  ? final_camera_spec(width, rn, rd)
+                                               : default_camera_spec(width, rn, rd, vfov, focal_length, aperture);
   if (int st = check_spec(c)) return st;
   *out = build_camera(c);
   return RT_OK;

@@ -1,7 +1,7 @@
 // main.cpp — ray-cli: the reference's CLI (src/main.rs, src/argparse.rs) on the C++ host, with
 // render_scene (main.rs:65-130) calling the MI355X render ABI instead of the rayon scanline loop.
 //
-//   ray-cli [-v...] render <random|saved|demo|perlin|earth|box-light|cornell|spheres> [options]
+//   ray-cli [-v...] render <random|saved|demo|perlin|earth|box-light|cornell|spheres|final> [options]
 //   ray-cli test
 //
 // Reference flags (argparse.rs:106-167): -o/--output out.png, -s/--samples 100, -m/--max-reflect 50,
@@ -39,7 +39,7 @@ struct Args {
 [[noreturn]] void usage(const char* msg) {
   if (msg && *msg) std::fprintf(stderr, "error: %s\n", msg);
   std::fprintf(stderr,
-               "usage: ray-cli [-v] render <random|saved|demo|perlin|earth|box-light|cornell|spheres> [options]\n"
+               "usage: ray-cli [-v] render <random|saved|demo|perlin|earth|box-light|cornell|spheres|final> [options]\n"
                "       ray-cli test\n"
                "options: -o FILE -s N -m N -w N --single-threaded --camera-fov F --camera-focal-length F\n"
                "         --camera-aperture F --camera-aspect-ratio std3x2|std16x9|std16x10|square|target-iphone\n"

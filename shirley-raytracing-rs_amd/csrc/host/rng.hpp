@@ -15,6 +15,7 @@ namespace host {
 enum : uint32_t {
   kStreamRandomScene = 1,  // random_scene (scenes.rs:281-429)
   kStreamGenSpheres = 2,   // gen_spheres (benches/my_benchmark.rs:35-60)
+  kStreamFinalScene = 3,   // book-2 final_scene (extension; absent from the reference)
   kStreamPerlinBase = 16   // Perlin table j (perlin/mod.rs:73-85) uses stream 16 + j
 };
 

@@ -110,6 +110,33 @@ Material Material::fairy_light(TextureLoader t) {
   return m;
 }
 
+Material Material::isotropic(TextureLoader t) {
+  Material m;
+  m.kind = Isotropic;
+  m.tex = std::move(t);
+  return m;
+}
+
+Geometry Geometry::moving_sphere(Vec3 c0, Vec3 c1, double time0, double time1, double r) {
+  Geometry g;
+  g.kind = RT_GEOM_MOVING_SPHERE;
+  g.p[0] = c0.x; g.p[1] = c0.y; g.p[2] = c0.z; g.p[3] = r;
+  g.q[0] = c1.x; g.q[1] = c1.y; g.q[2] = c1.z; g.q[3] = time0; g.q[4] = time1;
+  return g;
+}
+Geometry Geometry::with_medium(double d) const {
+  Geometry g = *this;
+  g.medium = true;
+  g.density = d;
+  return g;
+}
+Geometry Geometry::with_transform(double deg, Vec3 off) const {
+  Geometry g = *this;
+  g.transform = true;
+  g.rotate_y = deg;
+  g.offset = off;
+  return g;
+}
 Geometry Geometry::sphere(Vec3 c, double r) {
   Geometry g;
   g.kind = RT_GEOM_SPHERE;
@@ -218,6 +245,12 @@ static Json geom_json(const Geometry& g) {
       o.set("xy_sides", xy).set("yz_sides", yz).set("xz_sides", xz);
       return tagged("RectBox", o);
     }
+    case RT_GEOM_MOVING_SPHERE: {
+      Json o = Json::object();
+      o.set("center0", jvec(Vec3(p[0], p[1], p[2]))).set("center1", jvec(Vec3(g.q[0], g.q[1], g.q[2])));
+      o.set("time0", Json::number(g.q[3])).set("time1", Json::number(g.q[4])).set("radius", Json::number(p[3]));
+      return tagged("MovingSphere", o);
+    }
   }
   return Json();
 }
@@ -231,6 +264,9 @@ static Geometry geom_parse(const Json& j) {
   if (tag == "RectYZ") return Geometry::yz_rect(rf("d1_min"), rf("d1_max"), rf("d2_min"), rf("d2_max"), rf("offset"));
   if (tag == "RectXZ") return Geometry::xz_rect(rf("d1_min"), rf("d1_max"), rf("d2_min"), rf("d2_max"), rf("offset"));
   if (tag == "RectBox") return Geometry::rect_box(pvec(p->at("min")), pvec(p->at("max")));
+  if (tag == "MovingSphere")
+    return Geometry::moving_sphere(pvec(p->at("center0")), pvec(p->at("center1")), rf("time0"), rf("time1"),
+                                   rf("radius"));
   throw std::runtime_error("unknown geometry variant `" + tag + "`");
 }
 
@@ -241,6 +277,7 @@ static Json mat_json(const Material& m) {
     case Material::Lambertian: return tagged("Lambertian", Json::object().set("albedo", tex_json(m.tex)));
     case Material::DiffuseLight: return tagged("DiffuseLight", Json::object().set("albedo", tex_json(m.tex)));
     case Material::FairyLight: return tagged("FairyLight", Json::object().set("albedo", tex_json(m.tex)));
+    case Material::Isotropic: return tagged("Isotropic", Json::object().set("albedo", tex_json(m.tex)));
   }
   return Json();
 }
@@ -260,6 +297,7 @@ static Material mat_parse(const Json& j) {
   if (tag == "Lambertian") return Material::lambertian(tex_parse(p->at("albedo")));
   if (tag == "DiffuseLight") return Material::diffuse_light(tex_parse(p->at("albedo")));
   if (tag == "FairyLight") return Material::fairy_light(tex_parse(p->at("albedo")));
+  if (tag == "Isotropic") return Material::isotropic(tex_parse(p->at("albedo")));
   throw std::runtime_error("unknown material variant `" + tag + "`");
 }
 
@@ -272,6 +310,9 @@ Json SceneBuilder::to_json() const {
   for (const auto& gm : objects) {
     Json o = Json::object();
     o.set("geometry", geom_json(gm.first)).set("material", mat_json(gm.second));
+    if (gm.first.medium) o.set("medium", Json::object().set("density", Json::number(gm.first.density)));
+    if (gm.first.transform)
+      o.set("transform", Json::object().set("rotate_y", Json::number(gm.first.rotate_y)).set("offset", jvec(gm.first.offset)));
     objs.push(o);
   }
   root.set("objects", objs);
@@ -289,7 +330,12 @@ SceneBuilder SceneBuilder::from_json(const Json& j) {
   else throw std::runtime_error("unknown skybox `" + sky + "`");
   const Json& objs = j.at("objects");
   if (objs.kind != Json::Array) throw std::runtime_error("`objects` must be an array");
-  for (const Json& o : objs.arr) b.add(geom_parse(o.at("geometry")), mat_parse(o.at("material")));
+  for (const Json& o : objs.arr) {
+    Geometry g = geom_parse(o.at("geometry"));
+    if (const Json* m = o.find("medium")) g = g.with_medium(m->at("density").as_number());
+    if (const Json* t = o.find("transform")) g = g.with_transform(t->at("rotate_y").as_number(), pvec(t->at("offset")));
+    b.add(g, mat_parse(o.at("material")));
+  }
   if (const Json* ps = j.find("perlin_seed")) {
     b.has_perlin_seed = true;
     b.perlin_seed = (uint64_t)ps->as_number();
@@ -532,8 +578,9 @@ SceneDesc SceneBuilder::finalize(uint64_t seed) const {
         rm.param = m.ir;
         break;
       default: {
-        rm.kind = m.kind == Material::Lambertian ? RT_MAT_LAMBERTIAN
+        rm.kind = m.kind == Material::Lambertian     ? RT_MAT_LAMBERTIAN
                   : m.kind == Material::DiffuseLight ? RT_MAT_DIFFUSE_LIGHT
+                  : m.kind == Material::Isotropic    ? RT_MAT_ISOTROPIC
                                                      : RT_MAT_FAIRY_LIGHT;
         std::string key = m.tex.key();
         auto it = manager.find(key);
@@ -549,7 +596,14 @@ SceneDesc SceneBuilder::finalize(uint64_t seed) const {
     rt_object o{};
     o.geometry = gm.first.kind;
     o.material = (int32_t)d.materials.size() - 1;
-    for (int k = 0; k < 6; ++k) o.p[k] = gm.first.p[k];
+    const Geometry& g = gm.first;
+    for (int k = 0; k < 6; ++k) o.p[k] = g.p[k];
+    for (int k = 0; k < 5; ++k) o.q[k] = g.q[k];
+    o.medium = g.medium ? 1 : 0;
+    o.density = g.density;
+    o.transform = g.transform ? 1 : 0;
+    o.rotate_y_deg = g.rotate_y;
+    o.offset[0] = g.offset.x; o.offset[1] = g.offset.y; o.offset[2] = g.offset.z;
     d.objects.push_back(o);
   }
   for (size_t i = 0; i < d.images.size(); ++i) d.images[i].rgb = d.image_pixels[i].data();

@@ -48,7 +48,7 @@ struct TextureLoader {
 
 // material/material_type.rs:20-27 (MaterialType<TextureLoader>)
 struct Material {
-  enum Kind { Metal, Dielectric, Lambertian, DiffuseLight, FairyLight } kind = Lambertian;
+  enum Kind { Metal, Dielectric, Lambertian, DiffuseLight, FairyLight, Isotropic } kind = Lambertian;
   Vec3 albedo;  // Metal
   double fuzz = 0, ir = 1;
   TextureLoader tex;  // Lambertian / DiffuseLight / FairyLight
@@ -57,12 +57,24 @@ struct Material {
   static Material lambertian(TextureLoader t);
   static Material diffuse_light(TextureLoader t);
   static Material fairy_light(TextureLoader t);
+  static Material isotropic(TextureLoader t);  // book-2 extension (absent from the reference)
 };
 
-// geometry/object.rs:9-16
+// geometry/object.rs:9-16, plus the book-2 extensions (absent from the reference):
+// MovingSphere, and the object wrappers ConstantMedium (this shape as the boundary) and
+// Translate(RotateY(.)) — serde JSON: "MovingSphere" geometry, "medium" / "transform" object keys.
 struct Geometry {
   int32_t kind = RT_GEOM_SPHERE;
   double p[6] = {0, 0, 0, 0, 0, 0};
+  double q[5] = {0, 0, 0, 0, 0};  // MovingSphere: center1 xyz, time0, time1
+  bool medium = false;            // ConstantMedium boundary
+  double density = 0;
+  bool transform = false;         // Translate(offset) . RotateY(rotate_y)
+  double rotate_y = 0;
+  Vec3 offset;
+  static Geometry moving_sphere(Vec3 c0, Vec3 c1, double time0, double time1, double r);
+  Geometry with_medium(double density) const;
+  Geometry with_transform(double rotate_y_deg, Vec3 offset) const;
   static Geometry sphere(Vec3 c, double r);
   static Geometry xy_rect(double d1_min, double d1_max, double d2_min, double d2_max, double offset);
   static Geometry yz_rect(double d1_min, double d1_max, double d2_min, double d2_max, double offset);

@@ -196,6 +196,41 @@ SceneBuilder gen_spheres_scene(uint64_t seed, int32_t side_len) {
   return scene;
 }
 
+// book 2 ("The Next Week") §10 final_scene, drawn from the scene stream in the book's order.
+SceneBuilder final_scene(uint64_t seed, int32_t n_ground, int32_t n_cluster) {
+  SceneRng rng(seed, kStreamFinalScene);
+  SceneBuilder scene;
+  scene.set_skybox(RT_SKY_NONE);  // background black
+  const Material ground = Material::lambertian(TextureLoader::solid(0.48, 0.83, 0.53));
+  for (int i = 0; i < n_ground; i++)
+    for (int j = 0; j < n_ground; j++) {
+      const double w = 100.0;
+      const double x0 = -1000.0 + i * w, z0 = -1000.0 + j * w, y0 = 0.0;
+      const double x1 = x0 + w, y1 = rng.random_real(1.0, 101.0), z1 = z0 + w;
+      scene.add(Geometry::rect_box(Vec3(x0, y0, z0), Vec3(x1, y1, z1)), ground);
+    }
+  scene.add(Geometry::xz_rect(123.0, 423.0, 147.0, 412.0, 554.0), Material::diffuse_light(TextureLoader::solid(7.0, 7.0, 7.0)));
+  const Vec3 center1(400.0, 400.0, 200.0);
+  const Vec3 center2 = center1 + Vec3(30.0, 0.0, 0.0);
+  scene.add(Geometry::moving_sphere(center1, center2, 0.0, 1.0, 50.0), Material::lambertian(TextureLoader::solid(0.7, 0.3, 0.1)));
+  scene.add(Geometry::sphere(Vec3(260.0, 150.0, 45.0), 50.0), Material::dielectric(1.5));
+  const double fuzz = 1.0;
+  scene.add(Geometry::sphere(Vec3(0.0, 150.0, 145.0), 50.0), Material::metal(Vec3(0.8, 0.8, 0.9), &fuzz));
+  const Geometry boundary = Geometry::sphere(Vec3(360.0, 150.0, 145.0), 70.0);
+  scene.add(boundary, Material::dielectric(1.5));
+  scene.add(boundary.with_medium(0.2), Material::isotropic(TextureLoader::solid(0.2, 0.4, 0.9)));
+  const Geometry mist = Geometry::sphere(Vec3(0.0, 0.0, 0.0), 5000.0);
+  scene.add(mist.with_medium(0.0001), Material::isotropic(TextureLoader::solid(1.0, 1.0, 1.0)));
+  scene.add(Geometry::sphere(Vec3(400.0, 200.0, 400.0), 100.0), Material::lambertian(TextureLoader::earth()));
+  scene.add(Geometry::sphere(Vec3(220.0, 280.0, 300.0), 80.0), Material::lambertian(TextureLoader::noise(0.1)));
+  const Material white = Material::lambertian(TextureLoader::solid(0.73, 0.73, 0.73));
+  for (int j = 0; j < n_cluster; j++) {
+    const double x = rng.random_real(0.0, 165.0), y = rng.random_real(0.0, 165.0), z = rng.random_real(0.0, 165.0);
+    scene.add(Geometry::sphere(Vec3(x, y, z), 10.0).with_transform(15.0, Vec3(-100.0, 270.0, 395.0)), white);
+  }
+  return scene;
+}
+
 // ---------------------------------------------------------------------------------------------
 rt_camera build_camera(const CameraSpec& s) {
   rt_camera c{};
@@ -222,6 +257,8 @@ rt_camera build_camera(const CameraSpec& s) {
   c.u[0] = u.x; c.u[1] = u.y; c.u[2] = u.z;
   c.v[0] = v.x; c.v[1] = v.y; c.v[2] = v.z;
   c.focus_length = s.override_focus ? s.focus_length : fl;
+  c.time0 = s.time0;
+  c.time1 = s.time1;
   return c;
 }
 
@@ -258,6 +295,18 @@ CameraSpec spheres_camera_spec(int32_t width, int32_t rn, int32_t rd) {
   return s;
 }
 
+// book 2 §10: lookfrom (478, 278, -600), lookat (278, 278, 0), vfov 40, aperture 0, focus 10,
+// shutter [0, 1] (the book's camera has no lens at aperture 0: no disk draws)
+CameraSpec final_camera_spec(int32_t width, int32_t rn, int32_t rd) {
+  CameraSpec s = default_camera_spec(width, rn, rd, 40.0, 1.0, 0.0);
+  s.has_aperture = false;
+  s.look_from = Vec3(478.0, 278.0, -600.0);
+  s.look_at = Vec3(278.0, 278.0, 0.0);
+  s.time0 = 0.0;
+  s.time1 = 1.0;
+  return s;
+}
+
 bool aspect_ratio_from_name(const std::string& n, int32_t* num, int32_t* den) {
   struct R {
     const char* name;
@@ -290,6 +339,19 @@ bool builtin_scene(const std::string& name, uint64_t seed, SceneBuilder* out, st
       return false;
     }
     *out = gen_spheres_scene(seed, side);
+  } else if (name.rfind("final", 0) == 0) {
+    // final[:n_ground[:n_cluster]] (book: 20 and 1000)
+    int g = 20, n = 1000;
+    if (name.size() > 6 && name[5] == ':') {
+      g = std::atoi(name.c_str() + 6);
+      const size_t c2 = name.find(':', 6);
+      if (c2 != std::string::npos) n = std::atoi(name.c_str() + c2 + 1);
+    }
+    if (g < 0 || g > 1000 || n < 0 || n > 1000000) {
+      *err = "final scene: n_ground in [0, 1000], n_cluster in [0, 1e6]";
+      return false;
+    }
+    *out = final_scene(seed, g, n);
   } else {
     *err = "unknown scene `" + name + "`";
     return false;

@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -59,7 +60,7 @@ struct rt_ctx {
   // scene
   bool have_scene = false;
   DScene scene{};
-  DevBuf nodes, nodes4, prims, mats, texs, perlin, images, texels;
+  DevBuf nodes, nodes4, prims, mats, texs, perlin, images, texels, exts;
   rt_scene_stats stats{};
   int blocks_per_cu = 0;
   int mk_threads = kTraceThreads;  // megakernel block size (kTraceThreadsWide: whole BVH in LDS)
@@ -129,8 +130,76 @@ int upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes) {
   return RT_OK;
 }
 
-// object -> leaf box, exactly the reference's bounding_box (sphere.rs:54-60, rect.rs:82-99, rect.rs:158-163)
+// Book-2 extension parameters of an object, shared by the bounding box and the
+// device record: RotateY's cos / sin (rotate_y.h: radians = degrees * pi / 180).
+bool is_extended(const rt_object& o) {
+  return o.geometry == RT_GEOM_MOVING_SPHERE || o.medium != 0 || o.transform != 0;
+}
+void rotate_y_cs(const rt_object& o, double& cs, double& sn) {
+  const double rad = o.rotate_y_deg * 3.14159265358979323846 / 180.0;
+  cs = std::cos(rad);
+  sn = std::sin(rad);
+}
+// moving_sphere.h center(time), the device's formula (the bounding box uses it at time0 and time1)
+void moving_center(const rt_object& o, double tm, double* c) {
+  const double s = (tm - o.q[3]) / (o.q[4] - o.q[3]);
+  for (int k = 0; k < 3; ++k) c[k] = o.p[k] + (o.q[k] - o.p[k]) * s;
+}
+
+Box reference_box(const rt_object& o);
+// object -> leaf box: the reference's bounding_box for reference objects; for book-2 objects the
+// book's: moving_sphere.h (union of the boxes at time0 and time1), rotate_y.h (the 8 rotated
+// corners), translate (box + offset), constant_medium.h (the boundary's box).
 Box object_box(const rt_object& o) {
+  if (!is_extended(o)) return reference_box(o);
+  Box b{};
+  if (o.geometry == RT_GEOM_MOVING_SPHERE) {
+    double c0[3], c1[3];
+    moving_center(o, o.q[3], c0);
+    moving_center(o, o.q[4], c1);
+    Box b0{}, b1{};
+    for (int k = 0; k < 3; ++k) {
+      b0.mn[k] = c0[k] - o.p[3];
+      b0.mx[k] = c0[k] + o.p[3];
+      b1.mn[k] = c1[k] - o.p[3];
+      b1.mx[k] = c1[k] + o.p[3];
+    }
+    b = surrounding(b0, b1);
+  } else {
+    b = reference_box(o);
+  }
+  if (o.transform) {
+    double cs, sn;
+    rotate_y_cs(o, cs, sn);
+    Box r{};
+    for (int k = 0; k < 3; ++k) {
+      r.mn[k] = std::numeric_limits<double>::infinity();
+      r.mx[k] = -std::numeric_limits<double>::infinity();
+    }
+    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 2; ++j)
+        for (int k = 0; k < 2; ++k) {
+          const double x = i * b.mx[0] + (1 - i) * b.mn[0];
+          const double y = j * b.mx[1] + (1 - j) * b.mn[1];
+          const double z = k * b.mx[2] + (1 - k) * b.mn[2];
+          const double nx = cs * x + sn * z, nz = -sn * x + cs * z;
+          const double t[3] = {nx, y, nz};
+          for (int c = 0; c < 3; ++c) {
+            r.mn[c] = std::fmin(r.mn[c], t[c]);
+            r.mx[c] = std::fmax(r.mx[c], t[c]);
+          }
+        }
+    for (int k = 0; k < 3; ++k) {
+      r.mn[k] += o.offset[k];
+      r.mx[k] += o.offset[k];
+    }
+    b = r;
+  }
+  return b;
+}
+
+// exactly the reference's bounding_box (sphere.rs:54-60, rect.rs:82-99, rect.rs:158-163)
+Box reference_box(const rt_object& o) {
   Box b{};
   if (o.geometry == RT_GEOM_SPHERE) {
     for (int k = 0; k < 3; ++k) {
@@ -166,16 +235,23 @@ int validate(rt_ctx* c, const rt_scene_desc* d) {
   if (d->sky < RT_SKY_ABOVE || d->sky > RT_SKY_NONE) return fail(c, RT_E_INVALID, "bad skybox %d", d->sky);
   for (int i = 0; i < d->n_objects; ++i) {
     const rt_object& o = d->objects[i];
-    if (o.geometry < RT_GEOM_SPHERE || o.geometry > RT_GEOM_RECT_BOX)
+    if (o.geometry < RT_GEOM_SPHERE || o.geometry > RT_GEOM_MOVING_SPHERE)
       return fail(c, RT_E_INVALID, "object %d: bad geometry %d", i, o.geometry);
+    if ((o.medium != 0 && o.medium != 1) || (o.transform != 0 && o.transform != 1))
+      return fail(c, RT_E_INVALID, "object %d: medium / transform flags must be 0 or 1", i);
+    if (o.geometry == RT_GEOM_MOVING_SPHERE && !(o.q[4] != o.q[3]))
+      return fail(c, RT_E_INVALID, "object %d: moving sphere needs time0 != time1", i);
+    if (o.medium && (o.material < 0 || o.material >= d->n_materials || d->materials[o.material].kind != RT_MAT_ISOTROPIC))
+      return fail(c, RT_E_INVALID, "object %d: a constant medium takes an isotropic material", i);
     if (o.material < 0 || o.material >= d->n_materials)
       return fail(c, RT_E_INVALID, "object %d: material %d out of range", i, o.material);
   }
   for (int i = 0; i < d->n_materials; ++i) {
     const rt_material& m = d->materials[i];
-    if (m.kind < RT_MAT_METAL || m.kind > RT_MAT_FAIRY_LIGHT)
+    if (m.kind < RT_MAT_METAL || m.kind > RT_MAT_ISOTROPIC)
       return fail(c, RT_E_INVALID, "material %d: bad kind %d", i, m.kind);
-    bool textured = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT || m.kind == RT_MAT_FAIRY_LIGHT;
+    bool textured = m.kind == RT_MAT_LAMBERTIAN || m.kind == RT_MAT_DIFFUSE_LIGHT || m.kind == RT_MAT_FAIRY_LIGHT ||
+                    m.kind == RT_MAT_ISOTROPIC;
     if (textured && (m.texture < 0 || m.texture >= d->n_textures))
       return fail(c, RT_E_INVALID, "material %d: texture %d out of range", i, m.texture);
   }
@@ -348,7 +424,10 @@ void flatten4(const BuiltTree& t, const rt_scene_desc* d, double delta, std::vec
     set_child_box(out[it.parent], it.slot, &bn.box, delta);
     if (bn.leaf >= 0) {
       const int32_t g = d->objects[bn.leaf].geometry;
-      const int32_t flags = g == RT_GEOM_SPHERE ? 0 : (g == RT_GEOM_RECT_BOX ? kLeafGeneric | kLeafBox : kLeafGeneric);
+      // book-2 objects take the "box" (slow) leaf loop, which dispatches on the primitive
+      const int32_t flags = is_extended(d->objects[bn.leaf]) ? kLeafGeneric | kLeafBox
+                            : g == RT_GEOM_SPHERE            ? 0
+                            : (g == RT_GEOM_RECT_BOX ? kLeafGeneric | kLeafBox : kLeafGeneric);
       out[it.parent].child[it.slot] = ~(bn.leaf | flags);
       continue;
     }
@@ -520,6 +599,8 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
 
   WfParams P{};
   P.scene = c->wf_scene;
+  P.scene.time0 = kp.scene.time0;
+  P.scene.time1 = kp.scene.time1;
   P.cam = kp.cam;
   P.work = kp.work;
   wf_carve(c->wf_pool.p, n, P);
@@ -639,6 +720,8 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
 
   KParams kp{};
   kp.scene = c->scene;
+  kp.scene.time0 = cam->time0;  // book-2 shutter (ray time side stream)
+  kp.scene.time1 = cam->time1;
   kp.cam = device_camera(cam);
   kp.work.tiles_x = L.tiles_x;
   kp.work.tiles_y = L.tiles_y;
@@ -726,7 +809,7 @@ int rt_destroy(rt_ctx* c) {
   if (!c) return RT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->partial,
+  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->exts, &c->partial,
                     &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters})
     release(*b);
   for (auto& e : c->ev)
@@ -761,6 +844,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const Inflation infl = inflation_for(tree);
   flatten4(tree, d, infl.delta, nodes4, stack4);
   std::vector<DPrim> prims(std::max(1, d->n_objects));
+  std::vector<DExt> exts;
   for (int i = 0; i < d->n_objects; ++i) {
     const rt_object& o = d->objects[i];
     DPrim& q = prims[i];
@@ -770,8 +854,27 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
              : o.geometry == RT_GEOM_RECT_XY  ? kPrimRectXY
              : o.geometry == RT_GEOM_RECT_YZ  ? kPrimRectYZ
              : o.geometry == RT_GEOM_RECT_XZ  ? kPrimRectXZ
-                                              : kPrimBox;
+             : o.geometry == RT_GEOM_RECT_BOX ? kPrimBox
+                                              : kPrimMovingSphere;
     q.material = o.material;
+    if (is_extended(o)) {
+      if (exts.size() >= (1u << (31 - kPrimExtShift)))
+        return fail(c, RT_E_UNSUPPORTED, "too many extended objects");
+      DExt e{};
+      box_to6(object_box(o), e.box);
+      for (int k = 0; k < 3; ++k) e.c1[k] = o.q[k];
+      e.t0 = o.q[3];
+      e.t1 = o.q[4];
+      e.cos_t = 1.0;
+      if (o.transform) {
+        rotate_y_cs(o, e.cos_t, e.sin_t);
+        for (int k = 0; k < 3; ++k) e.off[k] = o.offset[k];
+      }
+      e.neg_inv_density = -1.0 / o.density;
+      q.kind |= kPrimExt | (o.medium ? kPrimMedium : 0) | (o.transform ? kPrimXform : 0) |
+                ((int32_t)exts.size() << kPrimExtShift);
+      exts.push_back(e);
+    }
   }
   std::vector<DMat> mats(std::max(1, d->n_materials));
   for (int i = 0; i < d->n_materials; ++i) {
@@ -821,6 +924,11 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   if ((st = upload(c, c->perlin, perl.data(), perl.size() * sizeof(DPerlin)))) return st;
   if ((st = upload(c, c->images, imgs.data(), imgs.size() * sizeof(DImage)))) return st;
   if ((st = upload(c, c->texels, texels.data(), texels.size()))) return st;
+  if (!exts.empty()) {
+    if ((st = upload(c, c->exts, exts.data(), exts.size() * sizeof(DExt)))) return st;
+  } else {
+    release(c->exts);
+  }
 
   DScene& S = c->scene;
   S.nodes = static_cast<const DNode*>(c->nodes.p);
@@ -841,6 +949,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.perlin = static_cast<const DPerlin*>(c->perlin.p);
   S.images = static_cast<const DImage*>(c->images.p);
   S.texels = static_cast<const uint8_t*>(c->texels.p);
+  S.exts = exts.empty() ? nullptr : static_cast<const DExt*>(c->exts.p);
+  S.time0 = S.time1 = 0.0;  // the shutter comes with each render call's camera
   S.n_nodes = (int32_t)nodes.size();
   S.n_prims = d->n_objects;
   int32_t depth = tree_branch_depth(tree);

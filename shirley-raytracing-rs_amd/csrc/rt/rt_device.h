@@ -147,6 +147,33 @@ __device__ __forceinline__ v3 random_in_unit_disk(Rng& r, uint64_t seed) {
   }
 }
 
+// One draw of a side stream (book-2 extensions): Philox4x32-10 at counter
+// (c0, sample, pixel, stream) with stream >= 2^30 — disjoint from the path streams (word 3 = 0) and
+// the scene streams (word 2 = 0xFFFFFFFF, small stream ids), so side draws never shift the
+// reference-order draws of a path.  Out of line and without philox10's SGPR pinning: it runs only
+// on extended primitives.
+constexpr uint32_t kStreamTime = 0x40000000u;    // the ray time of (pixel, sample)
+constexpr uint32_t kStreamMedium = 0x80000000u;  // | prim: a medium's free-flight draw, c0 = path draw index
+__device__ __noinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t sample, uint32_t pixel,
+                                         uint32_t stream) {
+  uint32_t c1 = sample, c2 = pixel, c3 = stream;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c0 = n0;
+    c1 = (uint32_t)p1;
+    c2 = n2;
+    c3 = (uint32_t)p0;
+  }
+  const uint64_t v = (uint64_t)c0 | ((uint64_t)c1 << 32);
+  return (double)(v >> 11) * (1.0 / 9007199254740992.0);
+}
+
 // ------------------------------------------------------------------------------------------
 // intersection (t only during traversal; the full hit record is rebuilt for the winner)
 // ------------------------------------------------------------------------------------------
@@ -263,8 +290,105 @@ __device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, 
   return face;
 }
 
-__device__ __forceinline__ bool prim_t(const DPrim& pr, v3 o, v3 d, double a, double t_min, double t_max, double& t,
+// ---- book-2 extensions (absent from the reference, parity unpinned) ----
+// A path's identity for the side streams: the counter-RNG coordinates of the ray being traced.
+__device__ __forceinline__ const DExt& prim_ext(const DScene& S, const DPrim& pr) {
+  return S.exts[pr.kind >> kPrimExtShift];
+}
+// camera.h get_ray (book 2): time = random_double(time0, time1), drawn from the path's time stream
+__device__ __forceinline__ double ray_time(double time0, double time1, uint32_t pixel, uint32_t sample,
+                                           uint64_t seed) {
+  return time0 + (time1 - time0) * side_draw(seed, 0u, sample, pixel, kStreamTime);
+}
+// moving_sphere.h center(time) = center0 + ((time - time0) / (time1 - time0)) * (center1 - center0)
+__device__ __forceinline__ v3 moving_center(const DPrim& pr, const DExt& e, double tm) {
+  const v3 c0 = V(pr.p[0], pr.p[1], pr.p[2]);
+  return c0 + scale(V(e.c1[0], e.c1[1], e.c1[2]) - c0, (tm - e.t0) / (e.t1 - e.t0));
+}
+// Translate::hit (moved origin o - offset) then RotateY::hit (origin and direction rotated by -angle)
+__device__ __forceinline__ void to_object(const DExt& e, int32_t kind, v3& o, v3& d) {
+  if (!(kind & kPrimXform)) return;
+  const v3 m = o - V(e.off[0], e.off[1], e.off[2]);
+  o = V(e.cos_t * m.x - e.sin_t * m.z, m.y, e.sin_t * m.x + e.cos_t * m.z);
+  d = V(e.cos_t * d.x - e.sin_t * d.z, d.y, e.sin_t * d.x + e.cos_t * d.z);
+}
+// The base shape of an extended primitive in its own frame (t only); tm = ray time.
+__device__ __forceinline__ bool base_t(const DPrim& pr, const DExt& e, int32_t base, v3 o, v3 d, double tm,
+                                       double t_min, double t_max, double& t, int& face) {
+  switch (base) {
+    case kPrimSphere: return sphere_t(pr.p, o, d, len2(d), t_min, t_max, t);
+    case kPrimMovingSphere: {
+      const v3 c = moving_center(pr, e, tm);
+      const double q[4] = {c.x, c.y, c.z, pr.p[3]};
+      return sphere_t(q, o, d, len2(d), t_min, t_max, t);
+    }
+    case kPrimRectXY: return rect_t<0, 1>(pr.p, o, d, t_min, t_max, t);
+    case kPrimRectYZ: return rect_t<1, 2>(pr.p, o, d, t_min, t_max, t);
+    case kPrimRectXZ: return rect_t<0, 2>(pr.p, o, d, t_min, t_max, t);
+    default: face = box_t(pr.p, o, d, t_min, t_max, t); return face >= 0;
+  }
+}
+// Closest-hit t of an extended primitive in [t_min, t_max] (after its leaf box passed).
+// constant_medium.h hit, restated so that the result does not depend on the running closest hit:
+// entry t1 (clamped to t_min, then 0) and exit t2 of the boundary; free flight
+// hd = neg_inv_density * ln(U), U from the medium stream keyed by (path draw index, prim); the
+// medium scatters at t1 + hd / |d| when hd <= (t2 - t1) |d| and that t is <= t_max.  (The book clamps
+// t2 to t_max first; the two agree in exact arithmetic, and this form makes the closest hit
+// independent of the order in which the traversal meets the primitives.)
+// Out of line (it runs only for book-2 primitives), with the path key passed by value: pixel,
+// sample and draw index of the path's stream, and the scene fields it reads (a reference into the
+// kernel's by-value parameter block would force the block into scratch memory).
+struct ExtHit {
+  double t;
+  int face;
+  int hit;
+};
+__device__ __noinline__ ExtHit ext_t(const DExt* exts, double time0, double time1, const DPrim pr, int prim, v3 o,
+                                     v3 d, double t_min, double t_max, uint32_t pixel, uint32_t sample,
+                                     uint32_t draw, uint64_t seed) {
+  ExtHit r{0.0, -1, 0};
+  const DExt& e = exts[pr.kind >> kPrimExtShift];
+  const int32_t kind = pr.kind, base = kind & kPrimBaseMask;
+  const double tm = base == kPrimMovingSphere ? ray_time(time0, time1, pixel, sample, seed) : 0.0;
+  to_object(e, kind, o, d);
+  if (!(kind & kPrimMedium)) {
+    r.hit = base_t(pr, e, base, o, d, tm, t_min, t_max, r.t, r.face) ? 1 : 0;
+    return r;
+  }
+  const double inf = __builtin_inf();
+  double t1, t2;
+  int f = -1;
+  if (!base_t(pr, e, base, o, d, tm, -inf, inf, t1, f)) return r;
+  if (!base_t(pr, e, base, o, d, tm, t1 + 0.0001, inf, t2, f)) return r;
+  if (t1 < t_min) t1 = t_min;
+  if (t1 >= t2) return r;
+  if (t1 < 0.0) t1 = 0.0;
+  const double ray_length = len(d);
+  const double inside = (t2 - t1) * ray_length;
+  const double hd = e.neg_inv_density * log(side_draw(seed, draw, sample, pixel, kStreamMedium | (uint32_t)prim));
+  if (hd > inside) return r;
+  const double th = t1 + hd / ray_length;
+  if (th > t_max) return r;
+  r.t = th;
+  r.face = -1;
+  r.hit = 1;
+  return r;
+}
+__device__ __forceinline__ bool ext_hit_t(const DScene& S, const DPrim& pr, int prim, v3 o, v3 d, double t_min,
+                                          double t_max, const Rng& rk, uint64_t seed, double& t, int& face) {
+  const ExtHit r = ext_t(S.exts, S.time0, S.time1, pr, prim, o, d, t_min, t_max, rk.pixel, rk.sample, rk.draw, seed);
+  if (r.hit) {
+    t = r.t;
+    face = r.face;
+  }
+  return r.hit != 0;
+}
+
+template <bool EXT>
+__device__ __forceinline__ bool prim_t(const DScene& S, const DPrim& pr, int prim, v3 o, v3 d, double a,
+                                       double t_min, double t_max, const Rng& rk, uint64_t seed, double& t,
                                        int& face) {
+  if (EXT && (pr.kind & kPrimExt)) return ext_hit_t(S, pr, prim, o, d, t_min, t_max, rk, seed, t, face);
   switch (pr.kind) {
     case kPrimSphere: return sphere_t(pr.p, o, d, a, t_min, t_max, t);
     case kPrimRectXY: return rect_t<0, 1>(pr.p, o, d, t_min, t_max, t);
@@ -342,6 +466,51 @@ __device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 
   finish_hit(h, d, normal);
 }
 
+// Hit record of an extended primitive, always with u, v: the base shape's record in its own frame
+// (a medium's: point r.at(t), normal (1, 0, 0), front face — constant_medium.h), then RotateY::hit
+// and Translate::hit map point and normal back to the world (front_face kept from the object frame,
+// as in the books' current edition).
+__device__ __noinline__ Hit ext_record(const DExt* exts, double time0, double time1, const DPrim pr, int face, v3 o,
+                                       v3 d, double t, uint32_t pixel, uint32_t sample, uint64_t seed) {
+  Hit h;
+  const DExt& e = exts[pr.kind >> kPrimExtShift];
+  const int32_t kind = pr.kind, base = kind & kPrimBaseMask;
+  to_object(e, kind, o, d);
+  if (kind & kPrimMedium) {
+    h.t = t;
+    h.point = o + scale(d, t);
+    h.normal = V(1.0, 0.0, 0.0);
+    h.front_face = true;
+    h.u = h.v = 0.0;
+  } else if (base == kPrimMovingSphere) {
+    const v3 c = moving_center(pr, e, ray_time(time0, time1, pixel, sample, seed));
+    h.t = t;
+    h.point = o + scale(d, t);
+    const v3 n = scale(h.point - c, 1.0 / pr.p[3]);
+    const UV uv = sphere_uv(n.x, n.y, n.z);
+    h.u = uv.u;
+    h.v = uv.v;
+    finish_hit(h, d, n);
+  } else {
+    DPrim q = pr;
+    q.kind = base;
+    prim_record<true>(q, face, o, d, t, h);
+  }
+  if (kind & kPrimXform) {
+    const v3 p = h.point, n = h.normal;
+    h.point = V(e.cos_t * p.x + e.sin_t * p.z, p.y, -e.sin_t * p.x + e.cos_t * p.z) + V(e.off[0], e.off[1], e.off[2]);
+    h.normal = V(e.cos_t * n.x + e.sin_t * n.z, n.y, -e.sin_t * n.x + e.cos_t * n.z);
+  }
+  return h;
+}
+// The winner's record: prim_record for reference primitives, ext_record for extended ones.
+template <bool WANT_UV, bool EXT>
+__device__ __forceinline__ void hit_record(const DScene& S, const DPrim& pr, int face, v3 o, v3 d, double t,
+                                           const Rng& rk, uint64_t seed, Hit& h) {
+  if (EXT && (pr.kind & kPrimExt)) h = ext_record(S.exts, S.time0, S.time1, pr, face, o, d, t, rk.pixel, rk.sample, seed);
+  else prim_record<WANT_UV>(pr, face, o, d, t, h);
+}
+
 // ------------------------------------------------------------------------------------------
 // BVH traversal: closest hit in [t_min, t_max] (bbox_tree.rs:56-91 semantics, near-first order)
 // ------------------------------------------------------------------------------------------
@@ -377,13 +546,14 @@ __device__ __forceinline__ const DNode& fetch_node(const DScene& S, const DNode*
 }
 
 // A leaf child whose (exact) box was hit: the object against the running closest (bbox_tree.rs:60-71).
+template <bool EXT>
 __device__ __forceinline__ void leaf_visit(const DScene& S, int prim, v3 o, v3 d, double t_min, Trav& T,
-                                           unsigned& ptests) {
+                                           const Rng& rk, uint64_t seed, unsigned& ptests) {
   const DPrim& pr = S.prims[prim];
   double t;
   int f = -1;
   ++ptests;
-  if (prim_t(pr, o, d, T.a, t_min, T.t_best, t, f)) {
+  if (prim_t<EXT>(S, pr, prim, o, d, T.a, t_min, T.t_best, rk, seed, t, f)) {
     T.t_best = t;
     T.best = prim;
     T.face = f;
@@ -395,9 +565,10 @@ __device__ __forceinline__ void leaf_visit(const DScene& S, int prim, v3 o, v3 d
 // child and push the farther.  Returns true when the traversal is complete (T.best / T.t_best /
 // T.face hold the closest hit).  Stack: per-lane, in LDS, [depth][lane] with a stride of the block
 // size (bank = lane % 32); entry t rounded down to f32 (only ever compared against t_best).
-template <int STRIDE, int MODE>
+template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_nodes, v3 o, v3 d, double t_min, Trav& T,
-                                          int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
+                                          const Rng& rk, uint64_t seed, int* stk_node, float* stk_t,
+                                          unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes) return true;  // defect guard: a traversal visits each node at most once
   const DNode& nd = fetch_node<MODE>(S, lds_nodes, T.node);
   const int c0 = nd.child[0], c1 = nd.child[1];
@@ -407,11 +578,11 @@ __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_node
   visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
   // leaf children (one primitive each)
   if (h0 && c0 < 0) {
-    leaf_visit(S, ~c0, o, d, t_min, T, ptests);
+    leaf_visit<EXT>(S, ~c0, o, d, t_min, T, rk, seed, ptests);
     h0 = false;
   }
   if (h1 && c1 < 0) {
-    leaf_visit(S, ~c1, o, d, t_min, T, ptests);
+    leaf_visit<EXT>(S, ~c1, o, d, t_min, T, rk, seed, ptests);
     h1 = false;
   }
   int next;
@@ -443,10 +614,10 @@ __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_node
 // HitList is always empty because every geometry is bounded).  Same visit order and tests as
 // trav_step, written as one loop over locals: the megakernel holds a whole path's state beside the
 // traversal, and this form keeps the traversal's registers out of scratch.
-template <int STRIDE, int MODE>
+template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes, v3 o, v3 d, double t_min,
-                                        double& t_best, int& face_best, int* stk_node, float* stk_t,
-                                        unsigned& visits, unsigned& ptests) {
+                                        double& t_best, int& face_best, const Rng& rk, uint64_t seed,
+                                        int* stk_node, float* stk_t, unsigned& visits, unsigned& ptests) {
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   const RaySigns ns = ray_signs(inv);
   const double a = len2(d);
@@ -465,7 +636,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
       double t;
       int f = -1;
       ++ptests;
-      if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = ~c0; face_best = f; }
+      if (prim_t<EXT>(S, pr, ~c0, o, d, a, t_min, t_best, rk, seed, t, f)) { t_best = t; best = ~c0; face_best = f; }
       h0 = false;
     }
     if (h1 && c1 < 0) {
@@ -473,7 +644,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
       double t;
       int f = -1;
       ++ptests;
-      if (prim_t(pr, o, d, a, t_min, t_best, t, f)) { t_best = t; best = ~c1; face_best = f; }
+      if (prim_t<EXT>(S, pr, ~c1, o, d, a, t_min, t_best, rk, seed, t, f)) { t_best = t; best = ~c1; face_best = f; }
       h1 = false;
     }
     int next;
@@ -650,11 +821,11 @@ __device__ __forceinline__ unsigned flag_mask(int c0, int c1, int c2, int c3, in
          ((((unsigned)~c3 >> b) & 1u) << 3);
 }
 
-template <int MODE>
+template <int MODE, bool EXT>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
                                             RaySigns ns, double a, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, double& t_best, float& tmaxf, int& best,
-                                            int& face_best, unsigned& ptests) {
+                                            int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
   // lm holds leaf children only
   const unsigned gm = flag_mask(c0, c1, c2, c3, 29), bm = flag_mask(c0, c1, c2, c3, 28);
   unsigned sph = lm & ~gm, rect = lm & gm & ~bm, box = lm & bm;
@@ -699,6 +870,13 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double te, t;
+    if (EXT && pr.kind != kPrimBox) {  // an extended primitive (book 2): exact box from its DExt record
+      if (!slab_s(prim_ext(S, pr).box, o, inv, ns, t_min, t_best, te)) continue;
+      ++ptests;
+      int f = -1;
+      if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
+      continue;
+    }
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
     ++ptests;
     const int f = box_t(pr.p, o, d, t_min, t_best, t);
@@ -722,11 +900,12 @@ __device__ __forceinline__ void cas_u(unsigned& a, unsigned& b) {
   a = lo;
   b = hi;
 }
-template <int STRIDE, int MODE>
+template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                       v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
-                                      unsigned* stk, unsigned& visits, unsigned& ptests) {
+                                      unsigned* stk, const Rng& rk, uint64_t seed, unsigned& visits,
+                                      unsigned& ptests) {
   PH_COUNT(0);
   const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
   const int4 ch = *reinterpret_cast<const int4*>(nd.child);
@@ -740,8 +919,8 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
                       (k2 < kInf && c2 < 0 ? 4u : 0u) | (k3 < kInf && c3 < 0 ? 8u : 0u);
   if (lm) PH_COUNT(1);
   if (lm)
-    leaf_tests4<MODE>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, tmaxf, best, face_best,
-                      ptests);
+    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, tmaxf, best, face_best,
+                      rk, seed, ptests);
   // internal children (0 <= c < kEmptyChild) as packed words; a miss (k = inf) packs above any bound
   const unsigned km = S.key_mask;
   unsigned p0 = (unsigned)c0 < (unsigned)kEmptyChild ? ((__float_as_uint(k0) & ~km) | (unsigned)c0) : ~0u;
@@ -771,10 +950,10 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
 // Whole closest-hit query over the 4-wide tree (t_min > 0).  The conservative internal tests and the
 // exact leaf tests make the set of primitives that can win the reference's (see DNode4F); the closest
 // hit is the reference's up to exact ties in t.
-template <int STRIDE, int MODE>
+template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                          double t_min, double& t_best, int& face_best, unsigned* stk,
-                                         unsigned& visits, unsigned& ptests
+                                         const Rng& rk, uint64_t seed, unsigned& visits, unsigned& ptests
 #ifdef RT_PHASE_TIMING
                                          , unsigned long long& trav_lane_steps_ref
 #endif
@@ -793,8 +972,8 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
 #ifdef RT_PHASE_TIMING
     ++g_trav_lane_steps;
 #endif
-    node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, tmaxf, best,
-                                face_best, sp, stk, visits, ptests);
+    node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, tmaxf, best,
+                                face_best, sp, stk, rk, seed, visits, ptests);
   }
   return best;
 }
@@ -824,13 +1003,13 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
 }
 
 // Returns true when the traversal is complete (T.best / T.t_best / T.face hold the closest hit).
-template <int STRIDE, int MODE>
+template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o,
-                                           v3 d, double t_min, Trav4& T, unsigned* stk, unsigned& visits,
-                                           unsigned& ptests) {
+                                           v3 d, double t_min, Trav4& T, unsigned* stk, const Rng& rk,
+                                           uint64_t seed, unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
-  T.node = visit4<STRIDE, MODE>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
-                                T.tmaxf, T.best, T.face, T.sp, stk, visits, ptests);
+  T.node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
+                                T.tmaxf, T.best, T.face, T.sp, stk, rk, seed, visits, ptests);
   return T.node < 0;
 }
 
@@ -1138,6 +1317,7 @@ __device__ __forceinline__ v3 image_texel(const DScene& S, const DTex& tx, doubl
 // outward normal is the record's normal un-flipped (negation is exact), and a rect's o1 + t d1 is
 // exactly the record's point component (x*y == y*x); the formulas are then prim_record's.
 __device__ __forceinline__ UV hit_uv(const DPrim& pr, int face, const Hit& h) {
+  if (pr.kind & kPrimExt) return UV{h.u, h.v};  // ext_record computed them
   if (pr.kind == kPrimSphere) {
     const v3 n = h.front_face ? h.normal : scale(h.normal, -1.0);
     return sphere_uv(n.x, n.y, n.z);
@@ -1255,6 +1435,12 @@ __device__ __forceinline__ bool shade(const DScene& S, const DPerlin* lds_perlin
     att = hmul(att, V(m.albedo[0], m.albedo[1], m.albedo[2]));
     return true;
   }
+  if (m.kind == RT_MAT_ISOTROPIC) {  // book-2 isotropic (extension): random_in_unit_sphere, albedo
+    att = hmul(att, texture_value(S, lds_perlin, m.tex, prim, face, h));
+    o = h.point;
+    d = r;
+    return true;
+  }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
   v3 a = texture_value(S, lds_perlin, m.tex, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
@@ -1299,6 +1485,12 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     o = h.point;
     d = reflected + scale(r, m.param);
     att = hmul(att, V(m.albedo[0], m.albedo[1], m.albedo[2]));
+    return true;
+  }
+  if (m.kind == RT_MAT_ISOTROPIC) {  // book-2 isotropic (extension): random_in_unit_sphere, albedo
+    att = hmul(att, leaf_texture_value(S, leaf, pn, prim, face, h));
+    o = h.point;
+    d = r;
     return true;
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)

@@ -58,7 +58,24 @@ enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2,
              kSceneLds = 3 };  // kSceneLds: all nodes AND all primitives in LDS (megakernel, small scenes)
 
 // Primitive kinds (device-side, rect axis folded into the kind).
-enum : int32_t { kPrimSphere = 0, kPrimRectXY = 1, kPrimRectYZ = 2, kPrimRectXZ = 3, kPrimBox = 4 };
+enum : int32_t { kPrimSphere = 0, kPrimRectXY = 1, kPrimRectYZ = 2, kPrimRectXZ = 3, kPrimBox = 4,
+                 kPrimMovingSphere = 5 };
+// Book-2 extensions (absent from the reference): DPrim.kind = base kind | flags |
+// (ext record index << kPrimExtShift).  Any extended primitive is a "slow" leaf (kLeafBox path).
+constexpr int32_t kPrimBaseMask = 0xff;
+constexpr int32_t kPrimMedium = 1 << 8;     // ConstantMedium with this shape as its boundary
+constexpr int32_t kPrimXform = 1 << 9;      // instance transform (RotateY then Translate)
+constexpr int32_t kPrimExt = 1 << 10;       // has a DExt record
+constexpr int kPrimExtShift = 11;
+// The extra parameters of an extended primitive (DScene.exts[kind >> kPrimExtShift]).
+struct alignas(16) DExt {
+  double box[6];            // the exact world bounding box (leaf box test), computed on the host
+  double c1[3], t0, t1;     // moving sphere: centre at t1 (centre at t0 = p[0..2]), motion interval
+  double cos_t, sin_t;      // RotateY: cos / sin of the angle in radians
+  double off[3];            // Translate offset
+  double neg_inv_density;   // ConstantMedium: -1 / density
+};
+static_assert(sizeof(DExt) == 144, "DExt layout");
 
 // One primitive = one reference leaf object (a RectBox stays ONE leaf of 6 faces, rect.rs:146-156).
 struct alignas(16) DPrim {
@@ -120,6 +137,8 @@ struct DScene {
                            // the f32 entry t with its low K bits replaced by the node index
   int32_t sky;
   double sky_color[3];
+  const DExt* exts;        // book-2 extension records (null when the scene has none)
+  double time0, time1;     // camera shutter (set per render call; moving spheres read it)
 };
 
 struct DCamera {

@@ -36,7 +36,9 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 
 // THREADS = kTraceThreads (several blocks per CU, 3 waves/SIMD) or kTraceThreadsWide (one block per
 // CU whose LDS holds the whole BVH next to the stacks); the register budget is 168 VGPRs either way.
-template <int THREADS, int MODE>
+// EXT: the scene has book-2 primitives; their out-of-line code is compiled into
+// separate instances so that reference scenes keep the kernel's register allocation.
+template <int THREADS, int MODE, bool EXT>
 __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
@@ -173,21 +175,22 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
     if (active) {
       ++n_seg;
 #ifdef RT_PHASE_TIMING
-      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, visits, ptests,
+      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits, ptests,
                                       ph_lane_steps);
       ph2 = clock64();
       ph_trav += ph2 - ph1;
 #else
-      prim = traverse4<THREADS, MODE>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, visits, ptests);
+      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
+                                      ptests);
 #endif
       if (prim >= 0) {
         hit = true;
         const DPrim pr = S.prims[prim];
-        prim_record<false>(pr, face, o, d, t_best, h);
+        hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
         mat = pr.material;
         mk = S.mats[mat].kind;
-        need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT;
-        if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT) {
+        need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
+        if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
           leaf = resolve_texture(S, S.mats[mat].tex, h.point);
           const DTex& tx = S.texs[leaf];
           if (tx.kind == RT_TEX_PERLIN) {
@@ -356,13 +359,16 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
   double t_best = t_max;
   int face = -1;
   unsigned visits = 0, ptests = 0;
-  int prim = traverse<kHitThreads, MODE>(S, lds_nodes, o, d, t_min, t_best, face, stk_node, stk_t, visits, ptests);
+  // side-stream key of a free ray (book-2 media): pixel = ray index, sample 0, draw 0, seed 0
+  const Rng rk{(uint32_t)i, 0u, 0u, 0u, 0u};
+  int prim = traverse<kHitThreads, MODE, true>(S, lds_nodes, o, d, t_min, t_best, face, rk, 0ull, stk_node, stk_t, visits,
+                                         ptests);
   HitOut r{};
   r.object = prim;
   if (prim >= 0) {
     const DPrim pr = S.prims[prim];
     Hit h;
-    prim_record(pr, face, o, d, t_best, h);
+    hit_record<true, true>(S, pr, face, o, d, t_best, rk, 0ull, h);
     r.front_face = h.front_face ? 1 : 0;
     r.t = h.t;
     r.point[0] = h.point.x; r.point[1] = h.point.y; r.point[2] = h.point.z;
@@ -391,14 +397,26 @@ static int node_mode4(const DScene& S) {
   return S.n_lds_nodes4 >= S.n_nodes4 ? kNodesLds : (S.n_lds_nodes4 == 0 ? kNodesGlobal : kNodesMixed);
 }
 
-template <int THREADS, int MODE>
-static hipError_t occupancy_impl(const DScene& S, int* blocks_per_cu) {
+template <int THREADS, int MODE, bool EXT>
+static hipError_t occupancy_impl1(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
   const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.n_lds_prims, S.n_lds_perlin, S.stack_depth4, THREADS);
-  hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE>,
+  hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE, EXT>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<THREADS, MODE>, THREADS, lds);
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<THREADS, MODE, EXT>, THREADS, lds);
+}
+template <int THREADS, int MODE>
+static hipError_t occupancy_impl(const DScene& S, int* blocks_per_cu) {
+  return S.exts ? occupancy_impl1<THREADS, MODE, true>(S, blocks_per_cu)
+                : occupancy_impl1<THREADS, MODE, false>(S, blocks_per_cu);
+}
+template <int THREADS, int MODE>
+static void launch_trace1(const KParams& p, int blocks, size_t lds, hipStream_t stream) {
+  if (p.scene.exts)
+    hipLaunchKernelGGL((trace_kernel<THREADS, MODE, true>), dim3(blocks), dim3(THREADS), lds, stream, p);
+  else
+    hipLaunchKernelGGL((trace_kernel<THREADS, MODE, false>), dim3(blocks), dim3(THREADS), lds, stream, p);
 }
 
 static hipError_t hit_prepare(const DScene& S) {
@@ -431,20 +449,15 @@ hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t s
   const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads);
   if (threads == kTraceThreadsWide) {
     if (p.scene.n_lds_prims > 0)
-      hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kSceneLds>), dim3(blocks), dim3(threads), lds, stream, p);
+      launch_trace1<kTraceThreadsWide, kSceneLds>(p, blocks, lds, stream);
     else
-      hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
+      launch_trace1<kTraceThreadsWide, kNodesLds>(p, blocks, lds, stream);
     return hipGetLastError();
   }
   switch (node_mode4(p.scene)) {
-    case kNodesLds:
-      hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesLds>), dim3(blocks), dim3(threads), lds, stream, p);
-      break;
-    case kNodesGlobal:
-      hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesGlobal>), dim3(blocks), dim3(threads), lds, stream, p);
-      break;
-    default:
-      hipLaunchKernelGGL((trace_kernel<kTraceThreads, kNodesMixed>), dim3(blocks), dim3(threads), lds, stream, p);
+    case kNodesLds: launch_trace1<kTraceThreads, kNodesLds>(p, blocks, lds, stream); break;
+    case kNodesGlobal: launch_trace1<kTraceThreads, kNodesGlobal>(p, blocks, lds, stream); break;
+    default: launch_trace1<kTraceThreads, kNodesMixed>(p, blocks, lds, stream);
   }
   return hipGetLastError();
 }

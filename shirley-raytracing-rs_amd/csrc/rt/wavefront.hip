@@ -57,7 +57,7 @@ __device__ __forceinline__ unsigned long long next_window(WfIter* it, int& q, ui
   return __shfl(base, 0);
 }
 
-template <int MODE>
+template <int MODE, bool EXT>
 __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
@@ -77,6 +77,7 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
   int slot = 0;
   v3 o = V(0, 0, 0), d = V(0, 0, 0);
   Trav T;
+  Rng rk{0u, 0u, 0u, 0u, 0u};  // side-stream key of the slot's path (read only when the scene has book-2 prims)
   unsigned visits = 0, ptests = 0, rays = 0;
   for (;;) {
     // lanes without a ray take the next slots of the wave's window
@@ -102,6 +103,7 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
           o = V(st.ox[slot], st.oy[slot], st.oz[slot]);
           d = V(st.dx[slot], st.dy[slot], st.dz[slot]);
           trav_begin(T, d, __builtin_inf());
+          if (S.exts) rk = Rng{st.pixel[slot], st.sample[slot], st.draw[slot], 0u, 0u};
           active = true;
           ++rays;
         }
@@ -111,7 +113,8 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
       if (exhausted) break;
       continue;
     }
-    if (active && trav_step<kExtendThreads, MODE>(S, lds_nodes, o, d, 0.001, T, stk_node, stk_t, visits, ptests)) {
+    if (active && trav_step<kExtendThreads, MODE, EXT>(S, lds_nodes, o, d, 0.001, T, rk, P.work.seed, stk_node, stk_t,
+                                                  visits, ptests)) {
       st.ht[slot] = T.t_best;
       st.hprim[slot] = T.best;
       st.hface[slot] = T.face;
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(kExtendThreads) void wf_extend(WfParams P) {
 // to the stacks (the megakernel's wide configuration).  Traversal then issues no global loads, and
 // each lane prefetches its NEXT ray (state, origin, direction) while it traverses the current one:
 // the refill latency (path state of 2 M slots lives in HBM) is hidden behind the traversal steps.
-template <int THREADS>
+template <int THREADS, bool EXT>
 __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
@@ -160,6 +163,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   v3 o = V(0, 0, 0), d = V(0, 0, 0), no = V(0, 0, 0), nd = V(0, 0, 0);
   Trav4 T;
   trav4_begin(T, S, V(0.0, 0.0, 0.0), V(1.0, 1.0, 1.0), 0.0);
+  Rng rk{0u, 0u, 0u, 0u, 0u};  // side-stream key of the slot's path (read only when the scene has book-2 prims)
   unsigned visits = 0, ptests = 0, rays = 0;
   for (;;) {
     // A. a lane without a ray takes its prefetched one (if that slot holds a ray)
@@ -170,6 +174,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
         o = no;
         d = nd;
         trav4_begin(T, S, o, d, __builtin_inf());
+        if (S.exts) rk = Rng{st.pixel[slot], st.sample[slot], st.draw[slot], 0u, 0u};
         active = true;
         ++rays;
       }
@@ -206,7 +211,8 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
       continue;
     }
     // C. one node visit for every lane holding a ray
-    if (active && trav4_step<THREADS, kSceneLds>(S, lds_nodes, lds_prims, o, d, 0.001, T, stk, visits, ptests)) {
+    if (active && trav4_step<THREADS, kSceneLds, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, T, stk, rk, P.work.seed, visits,
+                                                 ptests)) {
       st.ht[slot] = T.t_best;
       st.hprim[slot] = T.best;
       st.hface[slot] = T.face;
@@ -232,6 +238,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
 // ------------------------------------------------------------------------------------------
 // One lane per slot; the grid covers the slots exactly in whole waves (n_slots % 64 == 0), and the
 // wave of slot group g = slots [64 g, 64 g + 64) owns that group's unit window and texture queue.
+template <bool EXT>
 __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
   const DScene& S = P.scene;
   const DCamera& C = P.cam;
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
       const int face = st.hface[slot];
       const double t = st.ht[slot];
       Hit h;
-      prim_record<false>(pr, face, o, d, t, h);
+      hit_record<false, EXT>(S, pr, face, o, d, t, rng, seed, h);
       hp = h.point;
       const DMat m = S.mats[pr.material];
       if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
@@ -311,7 +318,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
             em = em + hmul(att, a);
           }
           alive = false;
-        } else {  // lambertian.rs:21-37 / lighting.rs:42-66
+        } else {  // lambertian.rs:21-37 / lighting.rs:42-66 / book-2 isotropic
           if (m.kind == RT_MAT_FAIRY_LIGHT) {
             double s = dot(h.normal, scale(d, -1.0));
             if (perlin) {
@@ -322,8 +329,11 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
             }
           }
           v3 r = random_in_unit_sphere(rng, seed);
-          v3 sc = h.normal + unit(r);
-          if (near_zero(sc)) sc = h.normal;
+          v3 sc = r;  // isotropic: the unit-ball point itself
+          if (m.kind != RT_MAT_ISOTROPIC) {
+            sc = h.normal + unit(r);
+            if (near_zero(sc)) sc = h.normal;
+          }
           o = h.point;
           d = sc;
           if (perlin) {
@@ -572,60 +582,69 @@ size_t wf_extend4_lds(const DScene& S) {
          (size_t)S.n_lds_perlin * sizeof(DPerlin) + (size_t)S.stack_depth4 * kTraceThreadsWide * kStack4EntryBytes;
 }
 
+// Kernel instances come in pairs: EXT = the scene has book-2 primitives (their out-of-line code
+// would otherwise cost every reference scene registers and scratch).
+template <class K>
+static hipError_t prepare_one(K kernel, int threads, int lds, int* blocks_per_cu) {
+  hipError_t e = hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+  if (e != hipSuccess) return e;
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, kernel, threads, lds);
+}
+
 // The 4-wide, scene-in-LDS extend kernel for scenes where the megakernel runs wide (`S` = that scene).
 hipError_t wf_prepare4(const DScene& S, int* extend_blocks_per_cu) {
   const int lds = (int)wf_extend4_lds(S);
-  hipError_t e = hipFuncSetAttribute((const void*)wf_extend4<kTraceThreadsWide>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-  if (e != hipSuccess) return e;
-  return hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend4<kTraceThreadsWide>,
-                                                       kTraceThreadsWide, lds);
+  return S.exts ? prepare_one(wf_extend4<kTraceThreadsWide, true>, kTraceThreadsWide, lds, extend_blocks_per_cu)
+                : prepare_one(wf_extend4<kTraceThreadsWide, false>, kTraceThreadsWide, lds, extend_blocks_per_cu);
 }
 
 hipError_t wf_launch_extend4(const WfParams& P, int extend_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(wf_extend4<kTraceThreadsWide>, dim3(extend_blocks), dim3(kTraceThreadsWide),
-                     wf_extend4_lds(P.scene), s, P);
+  const size_t lds = wf_extend4_lds(P.scene);
+  if (P.scene.exts)
+    hipLaunchKernelGGL((wf_extend4<kTraceThreadsWide, true>), dim3(extend_blocks), dim3(kTraceThreadsWide), lds, s, P);
+  else
+    hipLaunchKernelGGL((wf_extend4<kTraceThreadsWide, false>), dim3(extend_blocks), dim3(kTraceThreadsWide), lds, s, P);
   return hipGetLastError();
 }
 
+template <bool EXT>
+static hipError_t wf_prepare1(const DScene& S, int lds, int* extend_blocks_per_cu) {
+  switch (wf_mode(S)) {
+    case kNodesLds: return prepare_one(wf_extend<kNodesLds, EXT>, kExtendThreads, lds, extend_blocks_per_cu);
+    case kNodesGlobal: return prepare_one(wf_extend<kNodesGlobal, EXT>, kExtendThreads, lds, extend_blocks_per_cu);
+    default: return prepare_one(wf_extend<kNodesMixed, EXT>, kExtendThreads, lds, extend_blocks_per_cu);
+  }
+}
 hipError_t wf_prepare(const DScene& S, int* extend_blocks_per_cu) {
   const int lds = (int)wf_extend_lds(S.n_lds_nodes, S.stack_depth);
-  hipError_t e = hipSuccess;
-  switch (wf_mode(S)) {
-    case kNodesLds:
-      e = hipFuncSetAttribute((const void*)wf_extend<kNodesLds>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend<kNodesLds>, kExtendThreads, lds);
-      break;
-    case kNodesGlobal:
-      e = hipFuncSetAttribute((const void*)wf_extend<kNodesGlobal>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend<kNodesGlobal>, kExtendThreads, lds);
-      break;
-    default:
-      e = hipFuncSetAttribute((const void*)wf_extend<kNodesMixed>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(extend_blocks_per_cu, wf_extend<kNodesMixed>, kExtendThreads, lds);
-  }
-  return e;
+  return S.exts ? wf_prepare1<true>(S, lds, extend_blocks_per_cu) : wf_prepare1<false>(S, lds, extend_blocks_per_cu);
 }
 
 int wf_grid_threads() { return kGridThreads; }
 
 // One round = wf_launch_extend -> wf_launch_shade -> wf_launch_texture; `P.it` points at the
 // round's zeroed counters.
+template <bool EXT>
+static void wf_launch_extend1(const WfParams& P, int extend_blocks, size_t lds, hipStream_t s) {
+  switch (wf_mode(P.scene)) {
+    case kNodesLds: hipLaunchKernelGGL((wf_extend<kNodesLds, EXT>), dim3(extend_blocks), dim3(kExtendThreads), lds, s, P); break;
+    case kNodesGlobal: hipLaunchKernelGGL((wf_extend<kNodesGlobal, EXT>), dim3(extend_blocks), dim3(kExtendThreads), lds, s, P); break;
+    default: hipLaunchKernelGGL((wf_extend<kNodesMixed, EXT>), dim3(extend_blocks), dim3(kExtendThreads), lds, s, P);
+  }
+}
 hipError_t wf_launch_extend(const WfParams& P, int extend_blocks, hipStream_t s) {
   const size_t lds = wf_extend_lds(P.scene.n_lds_nodes, P.scene.stack_depth);
-  switch (wf_mode(P.scene)) {
-    case kNodesLds: hipLaunchKernelGGL(wf_extend<kNodesLds>, dim3(extend_blocks), dim3(kExtendThreads), lds, s, P); break;
-    case kNodesGlobal: hipLaunchKernelGGL(wf_extend<kNodesGlobal>, dim3(extend_blocks), dim3(kExtendThreads), lds, s, P); break;
-    default: hipLaunchKernelGGL(wf_extend<kNodesMixed>, dim3(extend_blocks), dim3(kExtendThreads), lds, s, P);
-  }
+  if (P.scene.exts) wf_launch_extend1<true>(P, extend_blocks, lds, s);
+  else wf_launch_extend1<false>(P, extend_blocks, lds, s);
   return hipGetLastError();
 }
 
+static void launch_shade1(const WfParams& P, int grid_blocks, hipStream_t s) {
+  if (P.scene.exts) hipLaunchKernelGGL(wf_shade<true>, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+  else hipLaunchKernelGGL(wf_shade<false>, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+}
 hipError_t wf_launch_shade(const WfParams& P, int grid_blocks, hipStream_t s) {
-  hipLaunchKernelGGL(wf_shade, dim3(grid_blocks), dim3(kGridThreads), 0, s, P);
+  launch_shade1(P, grid_blocks, s);
   return hipGetLastError();
 }
 
@@ -641,7 +660,7 @@ hipError_t wf_launch_texture(const WfParams& P, int grid_blocks, hipStream_t s) 
 hipError_t wf_start(const WfParams& P, int grid_blocks, hipStream_t s) {
   WfParams Q = P;
   Q.first = 1;
-  hipLaunchKernelGGL(wf_shade, dim3(grid_blocks), dim3(kGridThreads), 0, s, Q);
+  launch_shade1(Q, grid_blocks, s);
   return hipGetLastError();
 }
 

@@ -6,7 +6,8 @@ C ABI (libshirley_rt.so: HIP kernels for gfx950).  Module names mirror the refer
 """
 from ._native import LIB_DIR, BIN_DIR, RtError, rt_lib, host_lib  # noqa: F401
 from .scene import (SceneBuilder, Scene, TextureLoader, Metal, Dielectric, Lambertian, DiffuseLight,  # noqa: F401
-                    FairyLight, Sphere, RectBox, xy_rect, yz_rect, xz_rect, SkyBox, Vec3)
+                    FairyLight, Sphere, RectBox, xy_rect, yz_rect, xz_rect, SkyBox, Vec3,
+                    Isotropic, MovingSphere, ConstantMedium, Transform)
 from .camera import CameraBuilder, CameraPosition, default_camera, cornell_camera, scene_camera  # noqa: F401
 from .render import Device, RenderSettings, render_scene, to_image, write_png, tile_layout  # noqa: F401
 from . import scenes  # noqa: F401

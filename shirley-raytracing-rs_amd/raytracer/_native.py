@@ -15,7 +15,9 @@ BIN_DIR = os.path.join(_PKG_ROOT, "bin")
 
 RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_OOM, RT_E_UNSUPPORTED = 0, 1, 2, 3, 4
 RT_GEOM_SPHERE, RT_GEOM_RECT_XY, RT_GEOM_RECT_YZ, RT_GEOM_RECT_XZ, RT_GEOM_RECT_BOX = range(5)
+RT_GEOM_MOVING_SPHERE = 5  # book-2 extension
 RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_LAMBERTIAN, RT_MAT_DIFFUSE_LIGHT, RT_MAT_FAIRY_LIGHT = range(5)
+RT_MAT_ISOTROPIC = 5  # book-2 extension
 RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_IMAGE = range(4)
 RT_SKY_ABOVE, RT_SKY_FLAT, RT_SKY_NONE = range(3)
 RT_BVH_REFERENCE, RT_BVH_SAH = 0, 1
@@ -27,7 +29,10 @@ _d6 = C.c_double * 6
 
 
 class rt_object(C.Structure):
-    _fields_ = [("geometry", C.c_int32), ("material", C.c_int32), ("p", _d6)]
+    _fields_ = [("geometry", C.c_int32), ("material", C.c_int32), ("p", _d6),
+                # book-2 extensions (absent from the reference)
+                ("medium", C.c_int32), ("transform", C.c_int32), ("q", C.c_double * 5), ("density", C.c_double),
+                ("rotate_y_deg", C.c_double), ("offset", _d3)]
 
 
 class rt_material(C.Structure):
@@ -61,7 +66,7 @@ class rt_camera(C.Structure):
     _fields_ = [("image_width", C.c_int32), ("image_height", C.c_int32), ("height", C.c_double),
                 ("width", C.c_double), ("focal_length", C.c_double), ("has_lens", C.c_int32),
                 ("lens_radius", C.c_double), ("origin", _d3), ("w", _d3), ("u", _d3), ("v", _d3),
-                ("focus_length", C.c_double)]
+                ("focus_length", C.c_double), ("time0", C.c_double), ("time1", C.c_double)]
 
 
 class rt_render_params(C.Structure):
@@ -95,7 +100,8 @@ class sh_camera_spec(C.Structure):
     _fields_ = [("width", C.c_int32), ("ratio_num", C.c_int32), ("ratio_den", C.c_int32),
                 ("vfov", C.c_double), ("focal_length", C.c_double), ("has_aperture", C.c_int32),
                 ("aperture", C.c_double), ("look_from", _d3), ("look_at", _d3), ("up", _d3),
-                ("override_focus", C.c_int32), ("focus_length", C.c_double)]
+                ("override_focus", C.c_int32), ("focus_length", C.c_double),
+                ("time0", C.c_double), ("time1", C.c_double)]
 
 
 # every symbol declared in include/shirley_rt.h, with its C signature

@@ -34,6 +34,7 @@ class CameraBuilder:
     vfov: float = 1.0           # DEFAULT_FOCAL_LENGTH when unset (camera/mod.rs:46)
     focal_length: float = 1.0
     aperture: Optional[float] = None
+    shutter: Tuple[float, float] = (0.0, 0.0)  # book-2 extension: (time0, time1)
 
     def build(self, pos: CameraPosition) -> N.rt_camera:
         s = N.sh_camera_spec()
@@ -47,6 +48,7 @@ class CameraBuilder:
         s.up[:] = [float(x) for x in pos.up]
         s.override_focus = 0 if pos.focus_length is None else 1
         s.focus_length = 0.0 if pos.focus_length is None else float(pos.focus_length)
+        s.time0, s.time1 = float(self.shutter[0]), float(self.shutter[1])
         cam = N.rt_camera()
         N.host_check(N.host_lib().sh_camera_build(C.byref(s), C.byref(cam)))
         return cam

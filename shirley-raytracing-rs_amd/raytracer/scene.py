@@ -105,6 +105,15 @@ class FairyLight:
         return {"FairyLight": {"albedo": self.albedo.to_json()}}
 
 
+@dataclass
+class Isotropic:
+    """Book-2 extension (absent from the reference): a ConstantMedium's phase function."""
+    albedo: TextureLoader
+
+    def to_json(self):
+        return {"Isotropic": {"albedo": self.albedo.to_json()}}
+
+
 # ---- geometry (geometry/object.rs:9-16) -------------------------------------------------------
 @dataclass
 class Sphere:
@@ -160,6 +169,42 @@ class RectBox:
             "xz_sides": [_rect(p0.x, p1.x, p0.z, p1.z, p1.y), _rect(p0.x, p1.x, p0.z, p1.z, p0.y)]}}
 
 
+# ---- book-2 extensions (absent from the reference) ----------------------------
+@dataclass
+class MovingSphere:
+    """moving_sphere.h: centre center0 at time0 moving linearly to center1 at time1."""
+    center0: Vec3
+    center1: Vec3
+    time0: float
+    time1: float
+    radius: float
+
+    def to_json(self):
+        return {"MovingSphere": {"center0": _v(self.center0).to_json(), "center1": _v(self.center1).to_json(),
+                                 "time0": float(self.time0), "time1": float(self.time1),
+                                 "radius": float(self.radius)}}
+
+
+@dataclass
+class ConstantMedium:
+    """constant_medium.h: the object's geometry is the boundary of a medium of this density (its
+    material must be Isotropic)."""
+    density: float
+
+    def to_json(self):
+        return {"density": float(self.density)}
+
+
+@dataclass
+class Transform:
+    """translate(rotate_y(object, rotate_y), offset)."""
+    rotate_y: float = 0.0
+    offset: Vec3 = (0.0, 0.0, 0.0)
+
+    def to_json(self):
+        return {"rotate_y": float(self.rotate_y), "offset": _v(self.offset).to_json()}
+
+
 # ---- skybox (skybox/mod.rs:11-16) ------------------------------------------------------------
 class SkyBox:
     Above = ("Above", None)
@@ -206,8 +251,14 @@ class SceneBuilder:
         N.host_check(N.host_lib().sh_scene_set_skybox(self._h, kind, col))
         return self
 
-    def add(self, geometry, material) -> None:
-        obj = json.dumps({"geometry": geometry.to_json(), "material": material.to_json()})
+    def add(self, geometry, material, medium: Optional[ConstantMedium] = None,
+            transform: Optional[Transform] = None) -> None:
+        js = {"geometry": geometry.to_json(), "material": material.to_json()}
+        if medium is not None:
+            js["medium"] = medium.to_json()
+        if transform is not None:
+            js["transform"] = transform.to_json()
+        obj = json.dumps(js)
         N.host_check(N.host_lib().sh_scene_add_json(self._h, obj.encode()))
 
     def __len__(self):

@@ -3,7 +3,7 @@ from __future__ import annotations
 
 from .scene import SceneBuilder
 
-SCENES = ("random", "random-night", "demo", "perlin", "earth", "box-light", "cornell", "spheres")
+SCENES = ("random", "random-night", "demo", "perlin", "earth", "box-light", "cornell", "spheres", "final")
 
 
 def random_scene(seed: int = 0x5EED, night: bool = False) -> SceneBuilder:  # scenes.rs:281-429
@@ -34,3 +34,9 @@ def gen_spheres(seed: int = 0xDEADBEEF, side_len: int = 11) -> SceneBuilder:
     """benches/my_benchmark.rs:35-60 gen_spheres (22^3 = 10,648 spheres at side 11) with random book-1
     materials: the stand-in for BASELINE config 5 (no ~10k-primitive scene exists in the reference)."""
     return SceneBuilder.builtin(f"spheres:{side_len}", seed)
+
+
+def final_scene(seed: int = 0x5EED, n_ground: int = 20, n_cluster: int = 1000) -> SceneBuilder:
+    """Book 2 ("The Next Week") final_scene, BASELINE config 5: needs the book-2 extensions
+    (moving sphere, constant media, instance transform) that the reference does not have."""
+    return SceneBuilder.builtin(f"final:{n_ground}:{n_cluster}", seed)

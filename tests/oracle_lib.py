@@ -51,6 +51,7 @@ _SIGS = {
     "or_tree_node": (None, [C.c_void_p, C.c_int32, _d6, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
                             C.POINTER(C.c_int32)]),
     "or_scene_hit": (None, [C.c_void_p, _d6, C.c_double, C.c_double, C.POINTER(or_hit)]),
+    "or_scene_hit_at": (None, [C.c_void_p, _d6, C.c_double, C.c_double, C.c_uint32, C.POINTER(or_hit)]),
     "or_texture_value": (None, [C.c_void_p, C.c_int32, C.c_double, C.c_double, C.POINTER(C.c_double),
                                 C.POINTER(C.c_double)]),
     "or_perlin_noise": (C.c_double, [C.c_void_p, C.c_int32, C.POINTER(C.c_double)]),
@@ -100,9 +101,10 @@ class OracleScene:
             lib().or_scene_free(self.h)
             self.h = None
 
-    def hit(self, ray, t_min=0.001, t_max=float("inf")):
+    def hit(self, ray, t_min=0.001, t_max=float("inf"), index=0):
+        """Closest hit with rt_scene_hit's key for ray `index` (book-2 media draw from it)."""
         out = or_hit()
-        lib().or_scene_hit(self.h, d6(ray), t_min, t_max, C.byref(out))
+        lib().or_scene_hit_at(self.h, d6(ray), t_min, t_max, int(index), C.byref(out))
         return out
 
     def tree(self):

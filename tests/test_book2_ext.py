@@ -1,0 +1,158 @@
+"""Book-2 ("The Next Week") extensions: moving spheres, constant media, RotateY/Translate instances,
+the isotropic material and the book's final_scene (BASELINE config 5).
+
+None of these exist in the reference, so their parity is
+UNPINNED: these tests pin the oracle's restatement (oracle.c, "book-2 extensions") with analytic
+known answers, and pin the C++ host (bounding boxes, JSON, scene builder) against the oracle.
+The GPU parity tests (test_gpu_parity.py) then compare the HIP path with this oracle.
+"""
+import ctypes as C
+import json
+import math
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import raytracer as rt
+import raytracer._native as N
+
+L = O.lib
+
+
+def obj(geometry, p, q=None, medium=0, density=0.0, transform=0, rotate_y=0.0, offset=(0, 0, 0)):
+    o = N.rt_object(geometry=geometry, material=0)
+    o.p[:] = list(p) + [0.0] * (6 - len(p))
+    if q is not None:
+        o.q[:] = list(q)
+    o.medium, o.density, o.transform, o.rotate_y_deg = medium, density, transform, rotate_y
+    o.offset[:] = list(offset)
+    return o
+
+
+def hit(o, ray, t_min=0.001, t_max=float("inf")):
+    h = O.or_hit()
+    ok = L().or_object_hit(C.byref(o), O.d6(ray), t_min, t_max, C.byref(h))
+    return h if ok else None
+
+
+def bbox(o):
+    out = O._d6()
+    assert L().or_object_bbox(C.byref(o), out)
+    return list(out)
+
+
+def test_moving_sphere_at_ray_time():
+    # or_object_hit traces at time 0 (its key has time0 = time1 = 0): centre = center(0)
+    o = obj(N.RT_GEOM_MOVING_SPHERE, [-5, 0, -5, 1], q=[5, 0, -5, -1, 1])  # midpoint of [-1, 1] at time 0
+    h = hit(o, [0, 0, 0, 0, 0, -1])
+    assert h is not None and h.t == 4.0 and list(h.normal) == [0.0, 0.0, 1.0] and h.front_face == 1
+    o2 = obj(N.RT_GEOM_MOVING_SPHERE, [0, 0, -5, 1], q=[10, 0, -5, 0, 1])  # at centre0 at time 0
+    assert hit(o2, [0, 0, 0, 0, 0, -1]).t == 4.0
+    assert hit(o2, [3, 0, 0, 0, 0, -1]) is None
+
+
+def test_moving_sphere_bbox_is_union_over_motion():
+    o = obj(N.RT_GEOM_MOVING_SPHERE, [0, 0, 0, 2], q=[10, 4, 0, 0, 1])
+    assert bbox(o) == [-2, -2, -2, 12, 6, 2]
+
+
+def test_rotate_y_bbox_of_rotated_cube():
+    o = obj(N.RT_GEOM_RECT_BOX, [-1, -1, -1, 1, 1, 1], transform=1, rotate_y=45.0, offset=(10, 0, 0))
+    b = bbox(o)
+    s2 = math.sqrt(2.0)
+    assert np.allclose(b, [10 - s2, -1, -s2, 10 + s2, 1, s2], rtol=0, atol=1e-14)
+
+
+def test_translated_sphere_hit_record_in_world_space():
+    o = obj(N.RT_GEOM_SPHERE, [0, 0, 0, 1], transform=1, rotate_y=0.0, offset=(0, 0, -5))
+    h = hit(o, [0, 0, 0, 0, 0, -1])
+    assert h.t == 4.0 and list(h.point) == [0.0, 0.0, -4.0] and list(h.normal) == [0.0, 0.0, 1.0]
+
+
+def test_rotated_box_face_normal_rotates_back():
+    # unit cube rotated 90 deg about y: its +x face (normal (1,0,0)) ends up facing -z... any face a
+    # ray along -z from +z meets has a world normal close to (0, 0, 1)
+    o = obj(N.RT_GEOM_RECT_BOX, [-1, -1, -1, 1, 1, 1], transform=1, rotate_y=90.0)
+    h = hit(o, [0.2, 0.3, 5, 0, 0, -1])
+    assert abs(h.t - 4.0) < 1e-12 and np.allclose(list(h.normal), [0, 0, 1], atol=1e-12)
+    assert np.allclose(list(h.point), [0.2, 0.3, 1.0], atol=1e-12)
+
+
+def test_dense_medium_scatters_at_entry_and_thin_medium_never():
+    dense = obj(N.RT_GEOM_SPHERE, [0, 0, -5, 1], medium=1, density=1e300)
+    h = hit(dense, [0, 0, 0, 0, 0, -1])
+    assert h is not None and abs(h.t - 4.0) < 1e-12
+    assert list(h.normal) == [1.0, 0.0, 0.0] and h.front_face == 1  # constant_medium.h: arbitrary
+    thin = obj(N.RT_GEOM_SPHERE, [0, 0, -5, 1], medium=1, density=1e-300)
+    assert hit(thin, [0, 0, 0, 0, 0, -1]) is None
+    # starting inside: entry clamped to t_min
+    inside = hit(dense, [0, 0, -5, 0, 0, -1], t_min=0.001)
+    assert inside is not None and abs(inside.t - 0.001) < 1e-12
+    # beyond t_max: no hit
+    assert hit(dense, [0, 0, 0, 0, 0, -1], t_max=3.0) is None
+
+
+def test_medium_free_flight_is_exponential():
+    """hd = -ln(U)/density over many keys: mean free path 1/density (rt_scene_hit keys: ray index)."""
+    b = rt.SceneBuilder()
+    b.set_skybox(rt.SkyBox.Nothing)
+    b.add(rt.Sphere((0, 0, 0), 1000.0), rt.Isotropic(rt.TextureLoader.solid(1, 1, 1)), medium=rt.ConstantMedium(0.5))
+    osc = O.OracleScene(b.finalize())
+    ts = [osc.hit([0, 0, 0, 1, 0, 0], 0.0, float("inf"), index=i).t for i in range(4000)]
+    assert abs(np.mean(ts) - 2.0) < 0.15 and min(ts) >= 0.0
+
+
+def test_isotropic_scatter_is_unit_ball_point():
+    """Inside a dense medium an isotropic bounce leaves in a random_in_unit_sphere direction: the path
+    keeps scattering; with black sky and no lights the colour is exactly 0."""
+    b = rt.SceneBuilder()
+    b.set_skybox(rt.SkyBox.Nothing)
+    b.add(rt.Sphere((0, 0, 0), 50.0), rt.Isotropic(rt.TextureLoader.solid(0.5, 0.5, 0.5)), medium=rt.ConstantMedium(10.0))
+    osc = O.OracleScene(b.finalize())
+    cam = rt.CameraBuilder(width=4, aspect_ratio=(1, 1), vfov=10.0).build(rt.CameraPosition((0, 0, 0.5), (0, 0, -1)))
+    col, cnt = osc.sample(cam, O.params(1, 50), 1, 1, 0)
+    assert list(col) == [0.0, 0.0, 0.0] and cnt.segments == 50
+
+
+def test_json_round_trip_of_extensions():
+    b = rt.SceneBuilder()
+    b.add(rt.MovingSphere((0, 1, 2), (3, 4, 5), 0.0, 1.0, 0.5), rt.Lambertian(rt.TextureLoader.solid(1, 0, 0)))
+    b.add(rt.Sphere((0, 0, 0), 2.0), rt.Isotropic(rt.TextureLoader.solid(0.2, 0.4, 0.9)), medium=rt.ConstantMedium(0.2))
+    b.add(rt.RectBox((0, 0, 0), (1, 1, 1)), rt.Dielectric(1.5), transform=rt.Transform(15.0, (-100, 270, 395)))
+    js = json.loads(b.to_json())
+    o = js["objects"]
+    assert o[0]["geometry"]["MovingSphere"]["center1"] == {"vec": [3.0, 4.0, 5.0]}
+    assert o[1]["medium"] == {"density": 0.2} and "Isotropic" in o[1]["material"]
+    assert o[2]["transform"] == {"rotate_y": 15.0, "offset": {"vec": [-100.0, 270.0, 395.0]}}
+    assert rt.SceneBuilder.from_json(b.to_json()).to_json() == b.to_json()
+    d = b.finalize().desc
+    assert d.objects[0].geometry == N.RT_GEOM_MOVING_SPHERE and list(d.objects[0].q) == [3, 4, 5, 0, 1]
+    assert d.objects[1].medium == 1 and d.objects[1].density == 0.2
+    assert d.materials[1].kind == N.RT_MAT_ISOTROPIC
+    assert d.objects[2].transform == 1 and d.objects[2].rotate_y_deg == 15.0
+
+
+def test_final_scene_structure():
+    """book 2 §10: 20x20 ground boxes, light, moving sphere, glass, metal, glass + blue smoke,
+    mist, earth, marble, 1000 rotated + translated spheres."""
+    b = rt.scenes.final_scene(0x5EED)
+    assert len(b) == 400 + 1 + 1 + 1 + 1 + 2 + 1 + 1 + 1 + 1000
+    d = b.finalize(0x5EED).desc
+    objs = [d.objects[i] for i in range(d.n_objects)]
+    assert sum(o.geometry == N.RT_GEOM_RECT_BOX for o in objs) == 400
+    assert sum(o.geometry == N.RT_GEOM_MOVING_SPHERE for o in objs) == 1
+    assert sorted(o.density for o in objs if o.medium) == [0.0001, 0.2]
+    cluster = [o for o in objs if o.transform]
+    assert len(cluster) == 1000 and all(o.rotate_y_deg == 15.0 and list(o.offset) == [-100, 270, 395] for o in cluster)
+    assert all(0 <= o.p[k] <= 165 for o in cluster for k in range(3))
+    assert all(1.0 <= o.p[4] <= 101.0 for o in objs if o.geometry == N.RT_GEOM_RECT_BOX)
+    cam = rt.scene_camera("final", 100, "square")
+    assert (cam.time0, cam.time1, cam.has_lens) == (0.0, 1.0, 0)
+
+
+def test_final_scene_renders_on_oracle_with_light():
+    s = rt.scenes.final_scene(0x5EED, 4, 30).finalize(0x5EED)
+    cam = rt.scene_camera("final", 16, "square")
+    img, cnt = O.OracleScene(s).render(cam, O.params(4, 50, 0x5EED))
+    assert np.isfinite(img).all() and img.max() > 0 and cnt.samples == 16 * 16 * 4

@@ -76,7 +76,7 @@ def product_tree(desc_ptr, builder):
     return [(tuple(a.box), a.leaf, a.lhs, a.rhs) for a in arr[:n.value]], root.value
 
 
-@pytest.mark.parametrize("name", ["random", "random-night", "cornell", "demo", "earth"])
+@pytest.mark.parametrize("name", ["random", "random-night", "cornell", "demo", "earth", "final:6:60"])
 def test_reference_bvh_builder_equals_oracle(name):
     """O(N log N) builder (bvh_build.cpp) == literal restatement of constructor.rs (oracle.c)."""
     scene = rt.SceneBuilder.builtin(name, 0x5EED).finalize(0x5EED)
