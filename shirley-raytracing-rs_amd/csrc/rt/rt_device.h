@@ -1204,10 +1204,21 @@ __device__ __forceinline__ double unit_draw(uint64_t v) { return (double)(v >> 1
 __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, bool need) {
   v3 p = V(0.0, 0.0, 0.0);
   bool pending = false;
+  // A lane's own first attempt, with two Philox evaluations per wave instead of three: draws d, d+1,
+  // d+2 are halves of blocks d/2 and d/2 + 1, and an odd d takes its first draw from the cached odd
+  // half of block d/2 (three rng_next calls would each run Philox for the lanes at an even draw).
   if (need) {
-    const double x = random_real(r, seed, -1.0, 1.0);
-    const double y = random_real(r, seed, -1.0, 1.0);
-    const double z = random_real(r, seed, -1.0, 1.0);
+    const bool odd = (r.draw & 1u) != 0u;
+    uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+    if (!odd) philox_block(seed, r.pixel, r.sample, r.draw >> 1, a0, a1);
+    philox_block(seed, r.pixel, r.sample, (r.draw >> 1) + 1u, b0, b1);
+    const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
+    const double x = -1.0 + (1.0 - -1.0) * unit_draw(odd ? cached : a0);  // random_real(-1, 1), same ops
+    const double y = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b0 : a1);
+    const double z = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b1 : b0);
+    r.draw += 3u;
+    r.c2 = (uint32_t)b1;  // the odd half of block d/2 + 1, as the serial draws leave it
+    r.c3 = (uint32_t)(b1 >> 32);
     p = V(x, y, z);
     pending = !(len2(p) <= 1.0);
   }

@@ -113,13 +113,27 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void
       }
       if (need && idx < W.n_units) {
         // unit -> (local tile, chunk, lane-in-tile); tile-major so a window = 64 neighbours
-        unsigned long long per_tile = (unsigned long long)W.n_chunks * kTilePixels;
-        unsigned long long lt = idx / per_tile;
-        unsigned long long rem = idx - lt * per_tile;
+        unsigned long long lt, rem;
+        int tx, ty;
+        if (W.n_units <= 0xffffffffull) {  // wave-uniform: 32-bit quotients cost far less than 64-bit ones
+          const uint32_t pt = (uint32_t)W.n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
+          const uint32_t l32 = i32 / pt;
+          const uint32_t g32 = l32 * (uint32_t)W.tile_world + (uint32_t)W.tile_rank;
+          const uint32_t y32 = g32 / (uint32_t)W.tiles_x;
+          lt = l32;
+          rem = i32 - l32 * pt;
+          tx = (int)(g32 - y32 * (uint32_t)W.tiles_x);
+          ty = W.ty0 + (int)y32;
+        } else {
+          const unsigned long long per_tile = (unsigned long long)W.n_chunks * kTilePixels;
+          lt = idx / per_tile;
+          rem = idx - lt * per_tile;
+          const unsigned long long gt = lt * (unsigned long long)W.tile_world + (unsigned long long)W.tile_rank;
+          tx = (int)(gt % (unsigned long long)W.tiles_x);
+          ty = W.ty0 + (int)(gt / (unsigned long long)W.tiles_x);
+        }
         int chunk = (int)(rem / kTilePixels);
         int lp = (int)(rem % kTilePixels);
-        unsigned long long gt = lt * (unsigned long long)W.tile_world + (unsigned long long)W.tile_rank;
-        int tx = (int)(gt % (unsigned long long)W.tiles_x), ty = W.ty0 + (int)(gt / (unsigned long long)W.tiles_x);
         px = tx * kTile + (lp % kTile);
         py = ty * kTile + (lp / kTile);
         if (px < C.width && py < C.height) {

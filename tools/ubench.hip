@@ -40,6 +40,9 @@ __global__ __launch_bounds__(768) void kern(int n, unsigned long long* out, unsi
       if (OP == 16) asm volatile("v_min_f64 %0, %0, %0" : "+v"(f[i]));
       if (OP == 17) asm volatile("v_cmp_lt_f64 vcc, %0, %1" : : "v"(f[i]), "v"(f[(i + 1) % CHAINS]) : "vcc");
       if (OP == 18) asm volatile("ds_bpermute_b32 %0, %1, %0\n s_waitcnt lgkmcnt(0)" : "+v"(a[i]) : "v"(a[(i + 3) % CHAINS]));
+      if (OP == 19) asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(a[i]) : "s"(k));
+      if (OP == 20) asm volatile("v_mul_f64 %0, %0, %0" : "+v"(f[i]));
+      if (OP == 21) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(a[i]) : "v"(f[i]));
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -77,16 +80,18 @@ int main(int argc, char** argv) {
   const char* names[] = {"v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mul_u32_u24", "v_xor_b32",
                          "v_fma_f64", "v_add_f64", "v_rcp_f64", "v_sqrt_f64", "v_fma_f32", "v_pk_fma_f32",
                          "v_div_scale_f64", "v_cndmask_b32", "v_cvt_f64_u32", "v_ldexp_f64", "v_readlane_b32",
-                         "v_min_f64", "v_cmp_lt_f64", "ds_bpermute+wait"};
-  double c[19];
+                         "v_min_f64", "v_cmp_lt_f64", "ds_bpermute+wait", "v_mad_u32_u24", "v_mul_f64",
+                         "v_cvt_f32_f64"};
+  double c[22];
   c[0] = run<0>(n, blocks, d, sink); c[1] = run<1>(n, blocks, d, sink); c[2] = run<2>(n, blocks, d, sink);
   c[3] = run<3>(n, blocks, d, sink); c[4] = run<4>(n, blocks, d, sink); c[5] = run<5>(n, blocks, d, sink);
   c[6] = run<6>(n, blocks, d, sink); c[7] = run<7>(n, blocks, d, sink); c[8] = run<8>(n, blocks, d, sink);
   c[9] = run<9>(n, blocks, d, sink); c[10] = run<10>(n, blocks, d, sink); c[11] = run<11>(n, blocks, d, sink);
   c[12] = run<12>(n, blocks, d, sink); c[13] = run<13>(n, blocks, d, sink); c[14] = run<14>(n, blocks, d, sink);
   c[15] = run<15>(n, blocks, d, sink); c[16] = run<16>(n, blocks, d, sink); c[17] = run<17>(n, blocks, d, sink);
-  c[18] = run<18>(n, blocks, d, sink);
+  c[18] = run<18>(n, blocks, d, sink); c[19] = run<19>(n, blocks, d, sink); c[20] = run<20>(n, blocks, d, sink);
+  c[21] = run<21>(n, blocks, d, sink);
   printf("threads/block %d (%d waves per SIMD): SIMD cycles per wave-instruction\n", g_threads, g_threads / 256);
-  for (int i = 0; i < 19; ++i) printf("%-18s %6.2f\n", names[i], c[i]);
+  for (int i = 0; i < 22; ++i) printf("%-18s %6.2f\n", names[i], c[i]);
   return 0;
 }
