@@ -150,11 +150,10 @@ __device__ __forceinline__ v3 random_in_unit_disk(Rng& r, uint64_t seed) {
 // One draw of a side stream (book-2 extensions): Philox4x32-10 at counter
 // (c0, sample, pixel, stream) with stream >= 2^30 — disjoint from the path streams (word 3 = 0) and
 // the scene streams (word 2 = 0xFFFFFFFF, small stream ids), so side draws never shift the
-// reference-order draws of a path.  Out of line and without philox10's SGPR pinning: it runs only
-// on extended primitives.
+// reference-order draws of a path.  Without philox10's SGPR pinning (the key may live in VGPRs here).
 constexpr uint32_t kStreamTime = 0x40000000u;    // the ray time of (pixel, sample)
 constexpr uint32_t kStreamMedium = 0x80000000u;  // | prim: a medium's free-flight draw, c0 = path draw index
-__device__ __noinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t sample, uint32_t pixel,
+__device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t sample, uint32_t pixel,
                                          uint32_t stream) {
   uint32_t c1 = sample, c2 = pixel, c3 = stream;
   uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -335,15 +334,15 @@ __device__ __forceinline__ bool base_t(const DPrim& pr, const DExt& e, int32_t b
 // medium scatters at t1 + hd / |d| when hd <= (t2 - t1) |d| and that t is <= t_max.  (The book clamps
 // t2 to t_max first; the two agree in exact arithmetic, and this form makes the closest hit
 // independent of the order in which the traversal meets the primitives.)
-// Out of line (it runs only for book-2 primitives), with the path key passed by value: pixel,
-// sample and draw index of the path's stream, and the scene fields it reads (a reference into the
-// kernel's by-value parameter block would force the block into scratch memory).
+// Inlined into the EXT kernel instances only (out-of-line calls cost those instances ~300 B of
+// scratch per lane and 25 % of the book-2 final scene's throughput); the path key (pixel, sample,
+// draw index) and the scene fields it reads are passed by value.
 struct ExtHit {
   double t;
   int face;
   int hit;
 };
-__device__ __noinline__ ExtHit ext_t(const DExt* exts, double time0, double time1, const DPrim pr, int prim, v3 o,
+__device__ __forceinline__ ExtHit ext_t(const DExt* exts, double time0, double time1, const DPrim pr, int prim, v3 o,
                                      v3 d, double t_min, double t_max, uint32_t pixel, uint32_t sample,
                                      uint32_t draw, uint64_t seed) {
   ExtHit r{0.0, -1, 0};
@@ -470,7 +469,7 @@ __device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 
 // (a medium's: point r.at(t), normal (1, 0, 0), front face — constant_medium.h), then RotateY::hit
 // and Translate::hit map point and normal back to the world (front_face kept from the object frame,
 // as in the books' current edition).
-__device__ __noinline__ Hit ext_record(const DExt* exts, double time0, double time1, const DPrim pr, int face, v3 o,
+__device__ __forceinline__ Hit ext_record(const DExt* exts, double time0, double time1, const DPrim pr, int face, v3 o,
                                        v3 d, double t, uint32_t pixel, uint32_t sample, uint64_t seed) {
   Hit h;
   const DExt& e = exts[pr.kind >> kPrimExtShift];
