@@ -357,8 +357,28 @@ __device__ __forceinline__ ExtHit ext_t(const DExt* exts, double time0, double t
   const double inf = __builtin_inf();
   double t1, t2;
   int f = -1;
-  if (!base_t(pr, e, base, o, d, tm, -inf, inf, t1, f)) return r;
-  if (!base_t(pr, e, base, o, d, tm, t1 + 0.0001, inf, t2, f)) return r;
+  if (base == kPrimSphere || base == kPrimMovingSphere) {
+    // the two boundary hits of a sphere from one discriminant: exactly what the two sphere_t calls
+    // (t in [-inf, inf], then [t1 + 0.0001, inf]) return, each root tested like sphere_t tests it
+    const v3 c = base == kPrimSphere ? V(pr.p[0], pr.p[1], pr.p[2]) : moving_center(pr, e, tm);
+    const v3 oc = o - c;
+    const double a = len2(d), half_b = dot(oc, d), cc = len2(oc) - pr.p[3] * pr.p[3];
+    const double disc = half_b * half_b - a * cc;
+    if (disc < 0.0) return r;
+    const double sq = sqrt(disc);
+    const double r1 = (-half_b - sq) / a, r2 = (-half_b + sq) / a;
+    t1 = r1;  // sphere_t on [-inf, inf] accepts the first root whatever its value
+    const double lo = t1 + 0.0001;
+    if (r1 < lo || inf < r1) {
+      if (r2 < lo || inf < r2) return r;
+      t2 = r2;
+    } else {
+      t2 = r1;
+    }
+  } else {
+    if (!base_t(pr, e, base, o, d, tm, -inf, inf, t1, f)) return r;
+    if (!base_t(pr, e, base, o, d, tm, t1 + 0.0001, inf, t2, f)) return r;
+  }
   if (t1 < t_min) t1 = t_min;
   if (t1 >= t2) return r;
   if (t1 < 0.0) t1 = 0.0;

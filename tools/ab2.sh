@@ -3,6 +3,7 @@
 # (variant "main" = the in-tree build, else exp/<variant>).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+export SHIRLEY_ASSETS=${SHIRLEY_ASSETS:-$PWD/shirley-raytracing-rs_amd/assets}  # exp/<variant> libs resolve assets here
 i=0
 for spec in "$@"; do
   i=$((i+1))
