@@ -13,7 +13,7 @@
 //   * 4-wide collapsed BVH with conservative f32 child boxes (112-B DNode4F) and exact f64 leaf
 //     tests, nearest-first traversal, per-lane stack in LDS laid out [depth][lane] (conflict-free
 //     at any depth); for scenes that fit, the nodes, primitives and Perlin tables live in LDS too
-//     (one 768-thread block per CU);
+//     (one 1024-thread block per CU: 4 waves per SIMD at 128 VGPRs);
 //   * Perlin marble octaves and rejection-sampling attempts of a segment are dealt across the whole
 //     wave (marble_coop, random_in_unit_sphere_coop);
 //   * per-unit partial sums go to HBM once; a reduce kernel sums chunks in order (deterministic).
