@@ -65,6 +65,32 @@ def test_render_matches_oracle(gpu, name, width, aspect):
     assert np.array_equal(imgs["megakernel"], imgs["wavefront"])
 
 
+@pytest.mark.parametrize("name,aspect", [("random", "std16x9"), ("cornell", "square"), ("earth", "square"),
+                                         ("final:4:30", "square")])
+def test_render_matches_golden(gpu, name, aspect):
+    """The committed oracle fixtures (tests/golden/renders.npz, 32x32 @ 8 spp) as the reference data."""
+    import os
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "renders.npz"), allow_pickle=False)
+    key = name.replace(":", "_").replace("-", "_")
+    gpu.upload(rt.SceneBuilder.builtin(name, SEED).finalize(SEED))
+    img = gpu.render(rt.scene_camera(name, 32, aspect), rt.RenderSettings(samples=8, max_reflect=50, seed=SEED,
+                                                                          sample_chunk=8))
+    check_parity(img, gold[key], 8)
+
+
+def test_hit_queries_match_golden(gpu):
+    import os
+    gold = np.load(os.path.join(os.path.dirname(__file__), "golden", "hits.npz"), allow_pickle=False)
+    gpu.upload(rt.scenes.random_scene(SEED).finalize(SEED))
+    hits = gpu.hit(gold["rays"], 0.001, float("inf"))
+    for i in range(len(gold["rays"])):
+        assert hits[i].object == gold["object"][i]
+        if gold["object"][i] >= 0:
+            g = hits[i]
+            assert [g.t, *g.point, *g.normal] == list(gold["record"][i][:7])
+            assert abs(g.u - gold["record"][i][7]) < 1e-12 and abs(g.v - gold["record"][i][8]) < 1e-12
+
+
 @pytest.mark.parametrize("slots", ["64", "4096"])
 def test_wavefront_small_slot_pool(gpu, slots, monkeypatch):
     """Far fewer path slots than work units: every slot regenerates many paths and takes many
