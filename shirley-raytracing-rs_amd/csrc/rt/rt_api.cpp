@@ -701,16 +701,20 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   if (engine != RT_ENGINE_MEGAKERNEL && engine != RT_ENGINE_WAVEFRONT)
     return fail(c, RT_E_INVALID, "bad engine %d", p->engine);
 
-  // samples per unit: enough units to keep every resident lane busy ~16x over (tail < ~3%);
-  // the wavefront engine keeps units short (its slots regenerate every iteration anyway)
+  // samples per unit: ~80 units per resident lane, so that a wave's last units (its lanes finish
+  // at different times) cost little; but at least 8 samples per unit, whose fetch + partial-sum store
+  // then stay cheap (MI355X, headline frame: 16 units per lane 1600 Msamples/s, 60-110 -> 1735-1742,
+  // 240 at chunk 4 -> 1686).  The wavefront engine keeps units short (its slots regenerate every
+  // iteration anyway).
   int chunk = p->sample_chunk;
   if (chunk == 0 && engine == RT_ENGINE_WAVEFRONT) chunk = kWfDefaultChunk;
   if (chunk == 0) {
     long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
-    long long want_units = 16 * lanes;
+    long long want_units = 80 * lanes;
     long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
     n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
     chunk = (int)((samples + n_chunks - 1) / n_chunks);
+    chunk = std::max(chunk, std::min(8, samples));
   }
   chunk = std::max(1, std::min(chunk, samples));
   const int n_chunks = (samples + chunk - 1) / chunk;

@@ -1,3 +1,3 @@
-cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export SHIRLEY_ASSETS=$PWD/shirley-raytracing-rs_amd/assets
-SHIRLEY_LIB_DIR=$PWD/exp/ccam timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q  --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/parity_ccam.log 2>&1; rc=$?; echo "parity rc=$rc"; tail -2 gpurun_out/parity_slds.log; [ $rc -eq 0 ] || exit $rc
-AB_STEPS=5 bash tools/ab2.sh "prev;;" "ccam;;" "prev;;" "ccam;;" "prev;;" "ccam;;"
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?; echo "gpu tests rc=$rc"; tail -2 gpurun_out/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo --no-cpu > gpurun_out/bench_2rank.log 2>&1; echo "2-rank rc=$?"; grep metric gpurun_out/bench_2rank.log | cut -c1-300
