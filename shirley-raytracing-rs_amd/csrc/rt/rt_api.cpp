@@ -714,7 +714,10 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
     n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
     chunk = (int)((samples + n_chunks - 1) / n_chunks);
-    chunk = std::max(chunk, std::min(8, samples));
+    // raise short units towards 8 samples while that still leaves >= 32 units per lane (small
+    // frames keep their short units: there the tail is the larger cost)
+    const long long cap = n_pix > 0 ? (long long)samples * n_pix / (32 * lanes) : 0;
+    chunk = std::max(chunk, (int)std::min<long long>(8, cap));
   }
   chunk = std::max(1, std::min(chunk, samples));
   const int n_chunks = (samples + chunk - 1) / chunk;

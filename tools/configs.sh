@@ -12,5 +12,6 @@ run() {
 run cfg1 --scene random --width 400 --aspect std16x9 --spp 50
 run cfg3 --scene earth --width 800 --aspect square --spp 1000
 run cfg4 --scene cornell --width 600 --aspect square --spp 10000
+run cfg5_final --scene final --width 1920 --aspect std16x9 --spp 2000
 run cfg5_sah --scene spheres --width 1920 --aspect std16x9 --spp 16 --bvh sah
 run cfg5_ref --scene spheres --width 1920 --aspect std16x9 --spp 16 --bvh reference
