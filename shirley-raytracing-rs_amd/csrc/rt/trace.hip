@@ -34,13 +34,13 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
   return (size_t)n_lds_nodes * sizeof(DNode) + (size_t)stack_depth * stride * 8;
 }
 
-// THREADS = kTraceThreads (256-thread blocks, several per CU, at least 3 waves per SIMD: 168 VGPRs)
+// THREADS = kTraceThreads (256-thread blocks, several per CU, at least 4 waves per SIMD: 128 VGPRs)
 // or kTraceThreadsWide (one 1024-thread block per CU whose LDS holds the scene next to the stacks:
 // 4 waves per SIMD, 128 VGPRs).  HIP's second launch-bounds argument is the minimum waves per SIMD.
 // EXT: the scene has book-2 primitives; their code is compiled into separate
 // instances so that reference scenes keep the kernel's register allocation.
 template <int THREADS, int MODE, bool EXT>
-__global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 3) void trace_kernel(KParams P) {
+__global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
   DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
