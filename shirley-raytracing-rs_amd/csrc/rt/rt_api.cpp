@@ -982,7 +982,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
       (long long)S.stack_depth4 * kTraceThreadsWide * kStack4EntryBytes + (long long)nodes4.size() * sizeof(DNode4F);
   if (stack_bytes > kLdsBytes || stack4_bytes > kLdsBytes)
     return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
-  const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS);
+  const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS) &&
+                    !getenv("SHIRLEY_NO_WIDE");  // tuning
   c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
   S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
   S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4F), nodes4.size());
