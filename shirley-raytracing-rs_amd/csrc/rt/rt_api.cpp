@@ -720,6 +720,16 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     chunk = std::max(chunk, (int)std::min<long long>(8, cap));
   }
   chunk = std::max(1, std::min(chunk, samples));
+  if (engine == RT_ENGINE_MEGAKERNEL) {
+    // the megakernel indexes units and partial slots (n_pix * n_chunks) in 32 bits
+    const long long max_chunks = n_pix > 0 ? 0xffffffffLL / n_pix : samples;
+    if (max_chunks < 1) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
+    if ((samples + chunk - 1) / chunk > max_chunks) {
+      if (p->sample_chunk != 0)
+        return fail(c, RT_E_UNSUPPORTED, "sample_chunk %d: more than 2^32 work units", p->sample_chunk);
+      chunk = (int)((samples + max_chunks - 1) / max_chunks);
+    }
+  }
   const int n_chunks = (samples + chunk - 1) / chunk;
 
   st = ensure(c, c->partial, (size_t)std::max<long long>(1, n_pix * n_chunks * 3) * sizeof(double));

@@ -66,16 +66,17 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
   bool exhausted = false;
 
   // lane state
+  // (kept lean: every loop-carried VGPR here competes with the 128-VGPR budget of 4 waves per SIMD)
   bool has_unit = false, active = false;
-  int px = 0, py = 0, s_cur = 0, s_end = 0;
-  unsigned long long part_index = 0;  // partial-buffer slot of the unit
+  uint32_t pxy = 0;   // px | py << 16 of the unit's pixel (the host keeps width, height <= 65535)
+  int s_end = 0;      // the unit's samples are [.., s_end); the current one is rng.sample
+  uint32_t part_index = 0;  // partial-buffer slot of the unit (the host keeps slots < 2^32)
   v3 sum = V(0, 0, 0), o = V(0, 0, 0), d = V(0, 0, 0), att = V(0, 0, 0), em = V(0, 0, 0);
   int depth_left = 0;
   Rng rng{0, 0, 0, 0, 0};
-  unsigned long long n_seg = 0, n_samp = 0;
-  unsigned visits = 0, ptests = 0;
-  unsigned long long n_vis = 0, n_pt = 0;
-  const unsigned long long pix_per_chunk = (unsigned long long)W.n_tiles_rank * kTilePixels;
+  unsigned long long n_seg = 0, n_samp = 0;  // wave-uniform (SGPRs): popcounts of ballots
+  unsigned visits = 0, ptests = 0;           // per lane; flushed to the counters before 2^31
+  const uint32_t pix_per_chunk = (uint32_t)W.n_tiles_rank * (uint32_t)kTilePixels;
 
 #ifdef RT_PHASE_TIMING
   unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
@@ -85,8 +86,8 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
     const unsigned long long ph0 = clock64();
 #endif
     // 1. a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
-    if (has_unit && !active && s_cur >= s_end) {
-      double* dst = P.partial + part_index * 3;
+    if (has_unit && !active && rng.sample + 1u >= (uint32_t)s_end) {
+      double* dst = P.partial + (size_t)part_index * 3;
       dst[0] = sum.x;
       dst[1] = sum.y;
       dst[2] = sum.z;
@@ -113,53 +114,44 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
         if (nb >= W.n_units) exhausted = true;
       }
       if (need && idx < W.n_units) {
-        // unit -> (local tile, chunk, lane-in-tile); tile-major so a window = 64 neighbours
-        unsigned long long lt, rem;
-        int tx, ty;
-        if (W.n_units <= 0xffffffffull) {  // wave-uniform: 32-bit quotients cost far less than 64-bit ones
-          const uint32_t pt = (uint32_t)W.n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
-          const uint32_t l32 = i32 / pt;
-          const uint32_t g32 = l32 * (uint32_t)W.tile_world + (uint32_t)W.tile_rank;
-          const uint32_t y32 = g32 / (uint32_t)W.tiles_x;
-          lt = l32;
-          rem = i32 - l32 * pt;
-          tx = (int)(g32 - y32 * (uint32_t)W.tiles_x);
-          ty = W.ty0 + (int)y32;
-        } else {
-          const unsigned long long per_tile = (unsigned long long)W.n_chunks * kTilePixels;
-          lt = idx / per_tile;
-          rem = idx - lt * per_tile;
-          const unsigned long long gt = lt * (unsigned long long)W.tile_world + (unsigned long long)W.tile_rank;
-          tx = (int)(gt % (unsigned long long)W.tiles_x);
-          ty = W.ty0 + (int)(gt / (unsigned long long)W.tiles_x);
-        }
+        // unit -> (local tile, chunk, lane-in-tile); tile-major so a window = 64 neighbours.  32-bit
+        // quotients (the host keeps n_units < 2^32): far cheaper than 64-bit ones
+        const uint32_t pt = (uint32_t)W.n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
+        const uint32_t lt = i32 / pt;
+        const uint32_t g32 = lt * (uint32_t)W.tile_world + (uint32_t)W.tile_rank;
+        const uint32_t y32 = g32 / (uint32_t)W.tiles_x;
+        const uint32_t rem = i32 - lt * pt;
+        const int tx = (int)(g32 - y32 * (uint32_t)W.tiles_x);
+        const int ty = W.ty0 + (int)y32;
         int chunk = (int)(rem / kTilePixels);
         int lp = (int)(rem % kTilePixels);
-        px = tx * kTile + (lp % kTile);
-        py = ty * kTile + (lp / kTile);
+        const int px = tx * kTile + (lp % kTile);
+        const int py = ty * kTile + (lp / kTile);
         if (px < C.width && py < C.height) {
           has_unit = true;
-          s_cur = chunk * W.chunk;
-          s_end = min(W.samples, s_cur + W.chunk);
-          part_index = (unsigned long long)chunk * pix_per_chunk + lt * kTilePixels + (unsigned long long)lp;
+          const int s0 = chunk * W.chunk;
+          s_end = min(W.samples, s0 + W.chunk);
+          rng.sample = (uint32_t)s0 - 1u;  // advanced before each sample (wraps to s0)
+          rng.pixel = (uint32_t)py * (uint32_t)C.width + (uint32_t)px;
+          pxy = (uint32_t)px | ((uint32_t)py << 16);
+          part_index = (uint32_t)chunk * pix_per_chunk + lt * (uint32_t)kTilePixels + (uint32_t)lp;
           sum = V(0.0, 0.0, 0.0);
         }
       }
     }
     // 3. lanes between paths start the next sample (render.rs:60-65)
-    if (has_unit && !active && s_cur < s_end) {
-      rng.pixel = (uint32_t)py * (uint32_t)C.width + (uint32_t)px;
-      rng.sample = (uint32_t)s_cur;
+    const bool start = has_unit && !active && rng.sample + 1u < (uint32_t)s_end;
+    n_samp += __popcll(__ballot(start));
+    if (start) {
+      rng.sample += 1u;
       rng.draw = 0;
-      double jx = (double)px + rng_next(rng, seed);
-      double jy = (double)py + rng_next(rng, seed);
+      double jx = (double)(pxy & 0xffffu) + rng_next(rng, seed);
+      double jy = (double)(pxy >> 16) + rng_next(rng, seed);
       camera_ray(C, rng, seed, jx, jy, o, d);
       att = V(1.0, 1.0, 1.0);
       em = V(0.0, 0.0, 0.0);
       depth_left = W.max_depth;
       active = depth_left > 0;
-      ++s_cur;
-      ++n_samp;
       if (!active) sum = sum + em;  // max_depth == 0: ray_color returns black (render.rs:30)
     }
     if (!__any(active)) {
@@ -187,8 +179,8 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
     unsigned long long ph2 = ph1;
 #endif
     PH_COUNT(6);
+    n_seg += __popcll(__ballot(active));
     if (active) {
-      ++n_seg;
 #ifdef RT_PHASE_TIMING
       prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits, ptests,
                                       ph_lane_steps);
@@ -250,15 +242,16 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
       ph_wave_steps += dl;  // the wave's loop iterations = its slowest lane's steps
     }
 #endif
-    if (visits > (1u << 30)) { n_vis += visits; visits = 0; }
-    if (ptests > (1u << 30)) { n_pt += ptests; ptests = 0; }
+    if (visits > (1u << 30) || ptests > (1u << 30)) {  // (never within a frame of today's sizes)
+      DCounters* cs = P.counters + (blockIdx.x % kCounterSlots);
+      atomicAdd(&cs->node_visits, (unsigned long long)visits);
+      atomicAdd(&cs->prim_tests, (unsigned long long)ptests);
+      visits = ptests = 0;
+    }
   }
-  n_vis += visits;
-  n_pt += ptests;
-  // wave-reduce the counters, one atomic per wave
+  // wave-reduce the per-lane counters, one atomic per wave
+  unsigned long long n_vis = visits, n_pt = ptests;
   for (int off = 32; off > 0; off >>= 1) {
-    n_seg += __shfl_down(n_seg, off);
-    n_samp += __shfl_down(n_samp, off);
     n_vis += __shfl_down(n_vis, off);
     n_pt += __shfl_down(n_pt, off);
   }
