@@ -919,33 +919,33 @@ __device__ __forceinline__ void cas_u(unsigned& a, unsigned& b) {
   a = lo;
   b = hi;
 }
-template <int STRIDE, int MODE, bool EXT>
-__device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
-                                      v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
-                                      double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
-                                      unsigned* stk, const Rng& rk, uint64_t seed, unsigned& visits,
-                                      unsigned& ptests) {
+// visit4's node part: the f32 keys of `node`'s four children, its children, and the mask of hit
+// leaf children.
+template <int MODE>
+__device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* lds_nodes, v3 o, v3 inv,
+                                                const RayF& rf, double t_min, double t_best, float tmaxf, int node,
+                                                int4& ch, float& k0, float& k1, float& k2, float& k3,
+                                                unsigned& visits) {
   PH_COUNT(0);
   const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
-  const int4 ch = *reinterpret_cast<const int4*>(nd.child);
-  const int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+  ch = *reinterpret_cast<const int4*>(nd.child);
   const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
-  float k0, k1, k2, k3;
   node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
   const float kInf = __builtin_inff();
   visits += 4;
-  const unsigned lm = (k0 < kInf && c0 < 0 ? 1u : 0u) | (k1 < kInf && c1 < 0 ? 2u : 0u) |
-                      (k2 < kInf && c2 < 0 ? 4u : 0u) | (k3 < kInf && c3 < 0 ? 8u : 0u);
-  if (lm) PH_COUNT(1);
-  if (lm)
-    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, a, t_min, lm, c0, c1, c2, c3, t_best, tmaxf, best, face_best,
-                      rk, seed, ptests);
-  // internal children (0 <= c < kEmptyChild) as packed words; a miss (k = inf) packs above any bound
+  return (k0 < kInf && ch.x < 0 ? 1u : 0u) | (k1 < kInf && ch.y < 0 ? 2u : 0u) |
+         (k2 < kInf && ch.z < 0 ? 4u : 0u) | (k3 < kInf && ch.w < 0 ? 8u : 0u);
+}
+// visit4's ordering part: internal children as packed words (a miss, k = inf, packs above any
+// bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.
+template <int STRIDE>
+__device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, float k1, float k2, float k3,
+                                          float tmaxf, int& sp, unsigned* stk) {
   const unsigned km = S.key_mask;
-  unsigned p0 = (unsigned)c0 < (unsigned)kEmptyChild ? ((__float_as_uint(k0) & ~km) | (unsigned)c0) : ~0u;
-  unsigned p1 = (unsigned)c1 < (unsigned)kEmptyChild ? ((__float_as_uint(k1) & ~km) | (unsigned)c1) : ~0u;
-  unsigned p2 = (unsigned)c2 < (unsigned)kEmptyChild ? ((__float_as_uint(k2) & ~km) | (unsigned)c2) : ~0u;
-  unsigned p3 = (unsigned)c3 < (unsigned)kEmptyChild ? ((__float_as_uint(k3) & ~km) | (unsigned)c3) : ~0u;
+  unsigned p0 = (unsigned)ch.x < (unsigned)kEmptyChild ? ((__float_as_uint(k0) & ~km) | (unsigned)ch.x) : ~0u;
+  unsigned p1 = (unsigned)ch.y < (unsigned)kEmptyChild ? ((__float_as_uint(k1) & ~km) | (unsigned)ch.y) : ~0u;
+  unsigned p2 = (unsigned)ch.z < (unsigned)kEmptyChild ? ((__float_as_uint(k2) & ~km) | (unsigned)ch.z) : ~0u;
+  unsigned p3 = (unsigned)ch.w < (unsigned)kEmptyChild ? ((__float_as_uint(k3) & ~km) | (unsigned)ch.w) : ~0u;
   cas_u(p0, p1);
   cas_u(p2, p3);
   cas_u(p0, p2);
@@ -964,6 +964,22 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
     if (e <= lim) return (int)(e & km);
   }
   return -1;
+}
+template <int STRIDE, int MODE, bool EXT>
+__device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
+                                      v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
+                                      double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
+                                      unsigned* stk, const Rng& rk, uint64_t seed, unsigned& visits,
+                                      unsigned& ptests) {
+  int4 ch;
+  float k0, k1, k2, k3;
+  const unsigned lm = node4_visit<MODE>(S, lds_nodes, o, inv, rf, t_min, t_best, tmaxf, node, ch, k0, k1, k2, k3,
+                                        visits);
+  if (lm) PH_COUNT(1);
+  if (lm)
+    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, a, t_min, lm, ch.x, ch.y, ch.z, ch.w, t_best, tmaxf, best,
+                           face_best, rk, seed, ptests);
+  return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, stk);
 }
 
 // Whole closest-hit query over the 4-wide tree (t_min > 0).  The conservative internal tests and the
