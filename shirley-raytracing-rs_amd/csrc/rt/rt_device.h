@@ -940,7 +940,7 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* 
 // bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.
 template <int STRIDE>
 __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, float k1, float k2, float k3,
-                                          float tmaxf, int& sp, unsigned* stk) {
+                                          float tmaxf, int& sp, unsigned& top, unsigned* stk) {
   const unsigned km = S.key_mask;
   unsigned p0 = (unsigned)ch.x < (unsigned)kEmptyChild ? ((__float_as_uint(k0) & ~km) | (unsigned)ch.x) : ~0u;
   unsigned p1 = (unsigned)ch.y < (unsigned)kEmptyChild ? ((__float_as_uint(k1) & ~km) | (unsigned)ch.y) : ~0u;
@@ -952,25 +952,27 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   cas_u(p1, p3);
   cas_u(p1, p2);
   const unsigned lim = __float_as_uint(tmaxf) | km;  // tmaxf finite: inf entries fail
-  if (p3 <= lim) { stk[sp] = p3; sp += STRIDE; }
-  if (p2 <= lim) { stk[sp] = p2; sp += STRIDE; }
-  if (p1 <= lim) { stk[sp] = p1; sp += STRIDE; }
+  // the stack's top entry lives in `top` (~0u: empty); a push moves the old top to LDS (so stk[0]
+  // holds the ~0u sentinel under any pushed entry), a pop takes `top` and prefetches the next one
+  if (p3 <= lim) { stk[sp] = top; sp += STRIDE; top = p3; }
+  if (p2 <= lim) { stk[sp] = top; sp += STRIDE; top = p2; }
+  if (p1 <= lim) { stk[sp] = top; sp += STRIDE; top = p1; }
   if (p0 <= lim) return (int)(p0 & km);
-  while (sp > 0) {
+  for (;;) {
     PH_COUNT(5);
+    const unsigned e = top;
+    if (e == ~0u) return -1;
     sp -= STRIDE;
-    // a pushed subtree whose (lower-bound) entry lies beyond the current closest hit cannot hold it
-    const unsigned e = stk[sp];
+    top = stk[sp];
     if (e <= lim) return (int)(e & km);
   }
-  return -1;
 }
 template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                       v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
-                                      unsigned* stk, const Rng& rk, uint64_t seed, unsigned& visits,
-                                      unsigned& ptests) {
+                                      unsigned& top, unsigned* stk, const Rng& rk, uint64_t seed,
+                                      unsigned& visits, unsigned& ptests) {
   int4 ch;
   float k0, k1, k2, k3;
   const unsigned lm = node4_visit<MODE>(S, lds_nodes, o, inv, rf, t_min, t_best, tmaxf, node, ch, k0, k1, k2, k3,
@@ -979,7 +981,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
   if (lm)
     leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, a, t_min, lm, ch.x, ch.y, ch.z, ch.w, t_best, tmaxf, best,
                            face_best, rk, seed, ptests);
-  return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, stk);
+  return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
 }
 
 // Whole closest-hit query over the 4-wide tree (t_min > 0).  The conservative internal tests and the
@@ -1000,6 +1002,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
   float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;
+  unsigned top = ~0u;  // the stack's top entry (node4_next)
   int node = S.root4;
   // a tree traversal visits every node at most once: more steps than nodes can only be a defect,
   // and ends the loop instead of hanging the wave
@@ -1008,7 +1011,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
     ++g_trav_lane_steps;
 #endif
     node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, tmaxf, best,
-                                face_best, sp, stk, rk, seed, visits, ptests);
+                                face_best, sp, top, stk, rk, seed, visits, ptests);
   }
   return best;
 }
@@ -1019,6 +1022,7 @@ struct Trav4 {
   double a, t_best;
   float tmaxf;
   int best, face, node, sp, steps;
+  unsigned top;  // the stack's top entry (node4_next)
   RaySigns ns;
   RayF rf;
 };
@@ -1034,6 +1038,7 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
   T.face = -1;
   T.node = S.root4;
   T.sp = 0;
+  T.top = ~0u;
   T.steps = 0;
 }
 
@@ -1044,7 +1049,7 @@ __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_n
                                            uint64_t seed, unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
   T.node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
-                                T.tmaxf, T.best, T.face, T.sp, stk, rk, seed, visits, ptests);
+                                T.tmaxf, T.best, T.face, T.sp, T.top, stk, rk, seed, visits, ptests);
   return T.node < 0;
 }
 
