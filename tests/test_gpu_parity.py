@@ -328,6 +328,9 @@ def test_edge_cases(gpu, engine):
         gpu.render(cam, rt.RenderSettings(engine=engine, samples=-1))
     with pytest.raises(rt.RtError):
         gpu.render_scanlines(cam, rt.RenderSettings(engine=engine, samples=1), 5, 100)
+    if engine == "megakernel":  # 64 pixels x (2^26 + 1) one-sample units >= 2^32: refused before any work
+        with pytest.raises(rt.RtError, match="2\\^32"):
+            gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1))
 
 
 @pytest.mark.parametrize("engine", ENGINES)
