@@ -52,7 +52,7 @@ def _worker(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 5])  # 12 tiles: even, and uneven with padded ranks
 def test_two_rank_tile_gather_equals_single_frame(tmp_path, world):
     import random
     port = 29500 + random.randint(0, 2000)
