@@ -701,23 +701,21 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   if (engine != RT_ENGINE_MEGAKERNEL && engine != RT_ENGINE_WAVEFRONT)
     return fail(c, RT_E_INVALID, "bad engine %d", p->engine);
 
-  // samples per unit: ~80 units per resident lane, so that a wave's last units (its lanes finish
-  // at different times) cost little; but at least 8 samples per unit, whose fetch + partial-sum store
-  // then stay cheap (MI355X, headline frame: 16 units per lane 1600 Msamples/s, 60-110 -> 1735-1742,
-  // 240 at chunk 4 -> 1686).  The wavefront engine keeps units short (its slots regenerate every
-  // iteration anyway).
+  // samples per unit: ~256 units per resident lane, so that a wave's last units (its lanes finish at
+  // different times) cost little.  Short units only add partial-sum traffic (24 B written + read per
+  // unit), so the partial buffer is the only bound: <= 2 GiB.  (MI355X: headline frame chunk 23 -> 8
+  // +0.5 %, final_scene 19 -> 7 +5 %, gen_spheres @ 16 spp 3 -> 1 +24 %.)  The wavefront engine keeps
+  // its own unit length (its slots regenerate every iteration anyway).
   int chunk = p->sample_chunk;
   if (chunk == 0 && engine == RT_ENGINE_WAVEFRONT) chunk = kWfDefaultChunk;
   if (chunk == 0) {
-    long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
-    long long want_units = 80 * lanes;
+    const long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
+    const long long want_units = 256 * lanes;
     long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
+    const long long max_partial = 2LL << 30;  // bytes of [n_chunks][n_pix][3] f64
+    if (n_pix > 0) n_chunks = std::min<long long>(n_chunks, max_partial / (n_pix * 3 * (long long)sizeof(double)));
     n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
     chunk = (int)((samples + n_chunks - 1) / n_chunks);
-    // raise short units towards 8 samples while that still leaves >= 32 units per lane (small
-    // frames keep their short units: there the tail is the larger cost)
-    const long long cap = n_pix > 0 ? (long long)samples * n_pix / (32 * lanes) : 0;
-    chunk = std::max(chunk, (int)std::min<long long>(8, cap));
   }
   chunk = std::max(1, std::min(chunk, samples));
   if (engine == RT_ENGINE_MEGAKERNEL) {
