@@ -122,13 +122,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms, segments, laps = [], [], []
+    kernel_ms, segments, samples, laps = [], [], [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
         c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
         kernel_ms.append(c.kernel_ms)
         segments.append(c.segments)
+        samples.append(c.samples)
         laps.append((c.engine, c.iterations, c.slots, c.extend_ms, c.shade_ms, c.texture_ms, c.node_visits,
                      c.prim_tests))
     torch.cuda.synchronize()
@@ -148,7 +149,7 @@ def main():
     achieved = BYTES_PER_SEGMENT * seg / (k_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(REPO, "profiles", "traffic.json")
-    if os.path.exists(tfile):
+    if world == 1 and os.path.exists(tfile):  # (measured per N=1 launch; a rank's launch is smaller)
         try:
             tj = json.load(open(tfile))
             if tj.get("workload") == f"{args.scene} {W}x{H} @ {args.spp}spp" and tj.get("bvh") == args.bvh:
@@ -167,7 +168,7 @@ def main():
                    "slots": laps[-1][2],
                    "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
                                        "texture": round(laps[-1][5], 3)} if args.timing else None,
-                   "segments_per_sample": round(seg / (W * H * args.spp / world), 4) if world == 1 else None,
+                   "segments_per_sample": round(seg / max(float(np.mean(samples)), 1.0), 4),
                    "node_tests_per_segment": round(laps[-1][6] / max(seg, 1), 3),
                    "prim_tests_per_segment": round(laps[-1][7] / max(seg, 1), 3)},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
