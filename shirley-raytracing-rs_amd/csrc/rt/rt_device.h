@@ -724,6 +724,7 @@ __device__ __forceinline__ const DNode4F& fetch_node4(const DScene& S, const DNo
 struct RayF {
   float ox, oy, oz, ix, iy, iz, oix, oiy, oiz;
   bool fast;  // max|o| <= origin_limit: the f32 test's error bound holds
+  int dx, dy, dz;  // 48 when 1/d < 0 on the axis (the near plane is the hi row of DNode4F), else 0
 };
 __device__ __forceinline__ RayF ray_f(const DScene& S, v3 o, v3 inv) {
   RayF r;
@@ -737,55 +738,61 @@ __device__ __forceinline__ RayF ray_f(const DScene& S, v3 o, v3 inv) {
   r.oiy = r.oy * r.iy;
   r.oiz = r.oz * r.iz;
   r.fast = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) <= (double)S.origin_limit;
+  r.dx = r.ix < 0.f ? 48 : 0;
+  r.dy = r.iy < 0.f ? 48 : 0;
+  r.dz = r.iz < 0.f ? 48 : 0;
   return r;
 }
 
 // Conservative tests of the four children of a 4-wide node: per child the entry t (a lower bound)
-// or +inf when missed; min/max slab form (a NaN from 0 * inf leaves the bound; inverted boxes pass —
-// both only widen).  The node's six box rows are loaded up front (six 16-B reads), the f32 slab
-// arithmetic runs two children per packed instruction (v_pk_fma_f32), and only a ray with a far
-// origin (max|o| > origin_limit: rare, divergent) re-evaluates the same boxes in f64 (exact arithmetic
-// on a superset box).
+// or +inf when missed.  The ray picks each axis's near and far plane rows by the sign of 1/d (six
+// 16-B reads, no per-child min / max), the f32 slab arithmetic runs two children per packed
+// instruction (v_pk_fma_f32), and only a ray with a far origin (max|o| > origin_limit: rare,
+// divergent) re-evaluates the same boxes in f64 (exact arithmetic on a superset box).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 f2(float a, float b) { return f32x2{a, b}; }
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 __device__ __forceinline__ void node4_keys(const DNode4F& nd, const RayF& r, v3 o, v3 inv, float tminf, float tmaxf,
                                            double t_min, double t_max, float& k0, float& k1, float& k2, float& k3) {
-  const float4 lx = *reinterpret_cast<const float4*>(nd.lo[0]);
-  const float4 ly = *reinterpret_cast<const float4*>(nd.lo[1]);
-  const float4 lz = *reinterpret_cast<const float4*>(nd.lo[2]);
-  const float4 hx = *reinterpret_cast<const float4*>(nd.hi[0]);
-  const float4 hy = *reinterpret_cast<const float4*>(nd.hi[1]);
-  const float4 hz = *reinterpret_cast<const float4*>(nd.hi[2]);
+  // the near / far plane rows picked per ray by the sign of 1/d (rows lo x y z at 0 16 32, hi x y z at
+  // 48 64 80): for 1/d >= 0, fma(lo, i, -o i) <= fma(hi, i, -o i) (the FMA rounds monotonically), so the
+  // pick equals the min / max of the two and each child needs only max3 / min3; a NaN (0 * inf) is
+  // dropped by max3 / min3 like by the min / max form; an inverted box (lo > hi) now fails, which the
+  // exact test on it never passes either (its planes cross, so hit2 misses in that axis).
+  const char* nb = reinterpret_cast<const char*>(&nd);
+  const float4 nx4 = *reinterpret_cast<const float4*>(nb + r.dx);
+  const float4 fx4 = *reinterpret_cast<const float4*>(nb + (48 - r.dx));
+  const float4 ny4 = *reinterpret_cast<const float4*>(nb + (16 + r.dy));
+  const float4 fy4 = *reinterpret_cast<const float4*>(nb + (64 - r.dy));
+  const float4 nz4 = *reinterpret_cast<const float4*>(nb + (32 + r.dz));
+  const float4 fz4 = *reinterpret_cast<const float4*>(nb + (80 - r.dz));
   const f32x2 ix = f2(r.ix, r.ix), iy = f2(r.iy, r.iy), iz = f2(r.iz, r.iz);
   const f32x2 nx = f2(-r.oix, -r.oix), ny = f2(-r.oiy, -r.oiy), nz = f2(-r.oiz, -r.oiz);
   float key[4];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {  // children (2h, 2h + 1)
-    const f32x2 x0 = pk_fma(h ? f2(lx.z, lx.w) : f2(lx.x, lx.y), ix, nx);
-    const f32x2 x1 = pk_fma(h ? f2(hx.z, hx.w) : f2(hx.x, hx.y), ix, nx);
-    const f32x2 y0 = pk_fma(h ? f2(ly.z, ly.w) : f2(ly.x, ly.y), iy, ny);
-    const f32x2 y1 = pk_fma(h ? f2(hy.z, hy.w) : f2(hy.x, hy.y), iy, ny);
-    const f32x2 z0 = pk_fma(h ? f2(lz.z, lz.w) : f2(lz.x, lz.y), iz, nz);
-    const f32x2 z1 = pk_fma(h ? f2(hz.z, hz.w) : f2(hz.x, hz.y), iz, nz);
+  for (int h = 0; h < 2; ++h) {
+    const f32x2 x0 = pk_fma(h ? f2(nx4.z, nx4.w) : f2(nx4.x, nx4.y), ix, nx);
+    const f32x2 x1 = pk_fma(h ? f2(fx4.z, fx4.w) : f2(fx4.x, fx4.y), ix, nx);
+    const f32x2 y0 = pk_fma(h ? f2(ny4.z, ny4.w) : f2(ny4.x, ny4.y), iy, ny);
+    const f32x2 y1 = pk_fma(h ? f2(fy4.z, fy4.w) : f2(fy4.x, fy4.y), iy, ny);
+    const f32x2 z0 = pk_fma(h ? f2(nz4.z, nz4.w) : f2(nz4.x, nz4.y), iz, nz);
+    const f32x2 z1 = pk_fma(h ? f2(fz4.z, fz4.w) : f2(fz4.x, fz4.y), iz, nz);
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const float tn = fmaxf(fmaxf(fminf(x0[e], x1[e]), fminf(y0[e], y1[e])), fmaxf(fminf(z0[e], z1[e]), tminf));
-      const float tf = fminf(fminf(fmaxf(x0[e], x1[e]), fmaxf(y0[e], y1[e])), fminf(fmaxf(z0[e], z1[e]), tmaxf));
+      const float tn = fmaxf(fmaxf(x0[e], y0[e]), fmaxf(z0[e], tminf));
+      const float tf = fminf(fminf(x1[e], y1[e]), fminf(z1[e], tmaxf));
       key[2 * h + e] = tn <= tf ? tn : __builtin_inff();
     }
   }
   if (!r.fast) {  // far origins: the same inflated boxes in f64 (exact arithmetic on a superset box)
-    const float lo[3][4] = {{lx.x, lx.y, lx.z, lx.w}, {ly.x, ly.y, ly.z, ly.w}, {lz.x, lz.y, lz.z, lz.w}};
-    const float hi[3][4] = {{hx.x, hx.y, hx.z, hx.w}, {hy.x, hy.y, hy.z, hy.w}, {hz.x, hz.y, hz.z, hz.w}};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       double tn = t_min, tf = t_max;
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         const double iv = comp(inv, a), oa = comp(o, a);
-        const double t0 = ((double)lo[a][k] - oa) * iv, t1 = ((double)hi[a][k] - oa) * iv;
+        const double t0 = ((double)nd.lo[a][k] - oa) * iv, t1 = ((double)nd.hi[a][k] - oa) * iv;
         tn = fmax(tn, fmin(t0, t1));
         tf = fmin(tf, fmax(t0, t1));
       }
