@@ -762,11 +762,11 @@ __device__ __forceinline__ void node4_keys(const DNode4F& nd, const RayF& r, v3 
   // exact test on it never passes either (its planes cross, so hit2 misses in that axis).
   const char* nb = reinterpret_cast<const char*>(&nd);
   const float4 nx4 = *reinterpret_cast<const float4*>(nb + r.dx);
-  const float4 fx4 = *reinterpret_cast<const float4*>(nb + (48 - r.dx));
+  const float4 fx4 = *reinterpret_cast<const float4*>((nb - r.dx) + 48);
   const float4 ny4 = *reinterpret_cast<const float4*>(nb + (16 + r.dy));
-  const float4 fy4 = *reinterpret_cast<const float4*>(nb + (64 - r.dy));
+  const float4 fy4 = *reinterpret_cast<const float4*>((nb - r.dy) + 64);
   const float4 nz4 = *reinterpret_cast<const float4*>(nb + (32 + r.dz));
-  const float4 fz4 = *reinterpret_cast<const float4*>(nb + (80 - r.dz));
+  const float4 fz4 = *reinterpret_cast<const float4*>((nb - r.dz) + 80);
   const f32x2 ix = f2(r.ix, r.ix), iy = f2(r.iy, r.iy), iz = f2(r.iz, r.iz);
   const f32x2 nx = f2(-r.oix, -r.oix), ny = f2(-r.oiy, -r.oiy), nz = f2(-r.oiz, -r.oiz);
   float key[4];
@@ -948,11 +948,14 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* 
 template <int STRIDE>
 __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, float k1, float k2, float k3,
                                           float tmaxf, int& sp, unsigned& top, unsigned* stk) {
+  // No select needed for leaves and empty slots: a leaf's child word is negative (top bit set) and
+  // kEmptyChild is 0x7fffffff, so either word or-ed in packs above any limit (bits(tmaxf) | km <=
+  // 0x7f7fffff: tmaxf is finite and km < 2^20), as does a missed child's +inf key.
   const unsigned km = S.key_mask;
-  unsigned p0 = (unsigned)ch.x < (unsigned)kEmptyChild ? ((__float_as_uint(k0) & ~km) | (unsigned)ch.x) : ~0u;
-  unsigned p1 = (unsigned)ch.y < (unsigned)kEmptyChild ? ((__float_as_uint(k1) & ~km) | (unsigned)ch.y) : ~0u;
-  unsigned p2 = (unsigned)ch.z < (unsigned)kEmptyChild ? ((__float_as_uint(k2) & ~km) | (unsigned)ch.z) : ~0u;
-  unsigned p3 = (unsigned)ch.w < (unsigned)kEmptyChild ? ((__float_as_uint(k3) & ~km) | (unsigned)ch.w) : ~0u;
+  unsigned p0 = (__float_as_uint(k0) & ~km) | (unsigned)ch.x;
+  unsigned p1 = (__float_as_uint(k1) & ~km) | (unsigned)ch.y;
+  unsigned p2 = (__float_as_uint(k2) & ~km) | (unsigned)ch.z;
+  unsigned p3 = (__float_as_uint(k3) & ~km) | (unsigned)ch.w;
   cas_u(p0, p1);
   cas_u(p2, p3);
   cas_u(p0, p2);
