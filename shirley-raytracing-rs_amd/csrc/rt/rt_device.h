@@ -841,10 +841,10 @@ __device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
 }
 // f32 upper bound of a t: rounded up, and finite so that a +inf key (a miss) never passes `k <= tmaxf`
 __device__ __forceinline__ float tmax_f32(double t) { return fminf(__double2float_ru(t), 3.402823466e38f); }
-// 4-bit mask of the children whose ~child has bit `b` set
-__device__ __forceinline__ unsigned flag_mask(int c0, int c1, int c2, int c3, int b) {
-  return (((unsigned)~c0 >> b) & 1u) | ((((unsigned)~c1 >> b) & 1u) << 1) | ((((unsigned)~c2 >> b) & 1u) << 2) |
-         ((((unsigned)~c3 >> b) & 1u) << 3);
+// The top bytes of four words as one word, byte i = w_i >> 24 (two v_perm_b32 and an or).  Leaf
+// masks are kept in this "spread" form: bit 8 i + 7 stands for child i.
+__device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
+  return __builtin_amdgcn_perm(w1, w0, 0x0c0c0703u) | __builtin_amdgcn_perm(w3, w2, 0x07030c0cu);
 }
 
 template <int MODE, bool EXT>
@@ -852,14 +852,16 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
                                             RaySigns ns, double a, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, double& t_best, float& tmaxf, int& best,
                                             int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
-  // lm holds leaf children only
-  const unsigned gm = flag_mask(c0, c1, c2, c3, 29), bm = flag_mask(c0, c1, c2, c3, 28);
+  // lm: spread mask of hit leaf children (bit 8 i + 7: child i).  A leaf's child word is
+  // ~(prim | flags), so its generic / box flags (bits 29 / 28) are bits 5 / 4 of its top byte, inverted.
+  const unsigned nf = ~top_bytes((unsigned)c0, (unsigned)c1, (unsigned)c2, (unsigned)c3);
+  const unsigned gm = (nf << 2) & 0x80808080u, bm = (nf << 3) & 0x80808080u;
   unsigned sph = lm & ~gm, rect = lm & gm & ~bm, box = lm & bm;
   bool hit = false;
 #pragma unroll 1
   while (sph) {
     PH_COUNT(2);
-    const int k = __builtin_ctz(sph);
+    const int k = __builtin_ctz(sph) >> 3;
     sph &= sph - 1;
     const int leaf = ~child_at(k, c0, c1, c2, c3);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
@@ -872,7 +874,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
 #pragma unroll 1
   while (rect) {
     PH_COUNT(4);
-    const int k = __builtin_ctz(rect);
+    const int k = __builtin_ctz(rect) >> 3;
     rect &= rect - 1;
     const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
@@ -891,7 +893,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
 #pragma unroll 1
   while (box) {
     PH_COUNT(7);
-    const int k = __builtin_ctz(box);
+    const int k = __builtin_ctz(box) >> 3;
     box &= box - 1;
     const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
@@ -926,8 +928,8 @@ __device__ __forceinline__ void cas_u(unsigned& a, unsigned& b) {
   a = lo;
   b = hi;
 }
-// visit4's node part: the f32 keys of `node`'s four children, its children, and the mask of hit
-// leaf children.
+// visit4's node part: the f32 keys of `node`'s four children, its children, and the spread mask
+// (see top_bytes) of its hit leaf children.
 template <int MODE>
 __device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* lds_nodes, v3 o, v3 inv,
                                                 const RayF& rf, double t_min, double t_best, float tmaxf, int node,
@@ -938,10 +940,14 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* 
   ch = *reinterpret_cast<const int4*>(nd.child);
   const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
   node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
-  const float kInf = __builtin_inff();
   visits += 4;
-  return (k0 < kInf && ch.x < 0 ? 1u : 0u) | (k1 < kInf && ch.y < 0 ? 2u : 0u) |
-         (k2 < kInf && ch.z < 0 ? 4u : 0u) | (k3 < kInf && ch.w < 0 ? 8u : 0u);
+  // hit leaf: key < inf (bits(k) + 0x80800000 keeps the sign bit exactly for bits(k) < bits(inf); keys
+  // are >= 0) and a negative child word; as a spread mask
+  const unsigned h0 = (__float_as_uint(k0) + 0x80800000u) & (unsigned)ch.x;
+  const unsigned h1 = (__float_as_uint(k1) + 0x80800000u) & (unsigned)ch.y;
+  const unsigned h2 = (__float_as_uint(k2) + 0x80800000u) & (unsigned)ch.z;
+  const unsigned h3 = (__float_as_uint(k3) + 0x80800000u) & (unsigned)ch.w;
+  return top_bytes(h0, h1, h2, h3) & 0x80808080u;
 }
 // visit4's ordering part: internal children as packed words (a miss, k = inf, packs above any
 // bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.
