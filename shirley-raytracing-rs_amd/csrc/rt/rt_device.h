@@ -87,6 +87,10 @@ __device__ __forceinline__ v3 refract(v3 uv, v3 n, double eta) {
 struct Rng {
   uint32_t pixel, sample, draw, c2, c3;
 };
+// a ^ b ^ c in one instruction (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
                                          uint32_t k1) {
 #pragma unroll
@@ -102,7 +106,7 @@ __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     const uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-    uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    uint32_t n0 = xor3(hi1, c1, k0), n2 = xor3(hi0, c3, k1);
     c0 = n0;
     c1 = lo1;
     c2 = n2;
@@ -163,7 +167,7 @@ __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t
       k1 += 0xBB67AE85u;
     }
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
-    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0, n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0), n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c0 = n0;
     c1 = (uint32_t)p1;
     c2 = n2;
