@@ -107,7 +107,10 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
       } else {
         unsigned long long nb = 0;
         if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)kWave);
-        nb = __shfl(nb, 0);
+        // the whole wave is here (the loop's control flow is uniform), so lane 0 is the first active
+        // lane; readfirstlane (not a shuffle) lets the compiler keep the window in SGPRs
+        nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
+             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
         w_end = nb + kWave;
