@@ -23,7 +23,11 @@ sys.path.insert(0, os.path.join(REPO, "shirley-raytracing-rs_amd"))
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E peak (MI355X_MICROARCH.md, chip table)
 FP64_PEAK_TFLOPS = 78.6      # MI355X vector FP64 (spec)
-BYTES_PER_SEGMENT = 256      # algorithmic bytes per path segment, f64 path state
+# algorithmic bytes per path segment (SURVEY.md §8d contract): f32 path state 64 B read + 64 B
+# written + 8 B hit record written + 8 B read.  The graded roofline uses this figure.
+BYTES_PER_SEGMENT = 144
+# the same round trip for the reference's f64 path state, reported beside it
+BYTES_PER_SEGMENT_F64 = 256
 
 
 def parse():
@@ -42,22 +46,51 @@ def parse():
     ap.add_argument("--nodes", default="auto", choices=["auto", "global", "half-lds", "lds"], help="BVH node placement")
     ap.add_argument("--engine", default="auto", choices=["auto", "megakernel", "wavefront"])
     ap.add_argument("--timing", action="store_true", help="per-launch HIP-event timing of the wavefront kernels")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target wall time of the CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target wall time of each CPU-baseline leg (full frame at reduced spp; centre rows at full spp)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use (cgroup-aware)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     return ap.parse_args()
 
 
+def host_cpus():
+    """CPUs this process may run on: the affinity mask, capped by the cgroup CPU quota (a GPU box shares
+    its host: nproc reports the whole machine, the cgroup the box's share).  Returns (usable, info)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(quota)) if quota else aff)
+    model = "?"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return usable, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
+
+
 def cpu_baseline(scene, cam, args):
-    """The oracle (f64 C restatement, test infrastructure) timed on the host: full frame at reduced
-    spp (Msamples/s is per-sample throughput, so the spp reduction keeps the per-sample work)."""
+    """The oracle (f64 C restatement of the reference path, test infrastructure) timed on the host, on
+    every core this process may use (the rayon analogue: row-granular dynamic scheduling), two legs
+    (BASELINE.md): the full frame at reduced spp, and a centre band of rows at the full spp.
+    Msamples/s is per-sample throughput, so both are comparable with the GPU figure; `value` is the
+    full-frame leg (it weighs every pixel like the GPU frame)."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import oracle_lib as O
     osc = O.OracleScene(scene)
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
-    # calibrate on one sample per pixel, then size the measured sample to ~cpu_seconds of wall time
+    usable, info = host_cpus()
+    threads = args.cpu_threads or usable
+    W, H = cam.image_width, cam.image_height
+    # calibrate on one sample per pixel, then size each leg to ~cpu_seconds of wall time
     t0 = time.perf_counter()
     osc.render(cam, O.params(1, args.max_depth, args.seed + 1), threads=threads)
     per_spp = time.perf_counter() - t0
@@ -65,10 +98,42 @@ def cpu_baseline(scene, cam, args):
     t0 = time.perf_counter()
     _, cnt = osc.render(cam, O.params(spp, args.max_depth, args.seed), threads=threads)
     dt = time.perf_counter() - t0
-    return {"value": round(cnt.samples / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{args.scene} {cam.image_width}x{cam.image_height} @ {spp} spp (full frame, reduced spp; "
-                      f"{cnt.samples} samples, {dt:.1f} s wall on {threads} threads; f64 C oracle restating "
-                      f"the reference path, -O2)"}
+    full = cnt.samples / dt / 1e6
+    # centre band at full spp: rows sized from the full-frame rate
+    rows = int(max(1, min(H, round(args.cpu_seconds * full * 1e6 / (W * args.spp)))))
+    r0 = (H - rows) // 2
+    t0 = time.perf_counter()
+    _, cnt2 = osc.render(cam, O.params(args.spp, args.max_depth, args.seed), r0, r0 + rows, threads=threads)
+    dt2 = time.perf_counter() - t0
+    return {"value": round(full, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"{args.scene} {W}x{H} @ {spp} spp (full frame, reduced spp; {cnt.samples} samples, "
+                      f"{dt:.1f} s wall on {threads} threads; f64 C oracle restating the reference path, "
+                      f"-O2 -ffp-contract=off; a proxy: the Rust reference cannot be built here)",
+            "centre_rows_leg": {"value": round(cnt2.samples / dt2 / 1e6, 4), "unit": "Msamples/s",
+                                "sample": f"rows [{r0}, {r0 + rows}) x {W} @ {args.spp} spp (full spp), "
+                                          f"{cnt2.samples} samples, {dt2:.1f} s wall"},
+            "host": info}
+
+
+def valu_block(segments, k_ms, W, H, args):
+    """The measured ceiling of the trace kernel (VALU issue x lane utilisation), from the committed PMC
+    passes (profiles/valu.json, written by tools/pmc_valu.py from profiles/<round>/pmc_valu_*.csv of one
+    trace_kernel dispatch): per-segment instruction and f64-FLOP counts scaled by this run's segments
+    and kernel time."""
+    path = os.path.join(REPO, "profiles", "valu.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        v = json.load(open(path))
+    except (OSError, ValueError):
+        return None
+    if v.get("scene") != args.scene or v.get("bvh") != args.bvh or v.get("size") != [W, H]:
+        return None
+    flops = v["f64_flops_per_segment"] * segments
+    return {"bound": "valu", "busy_frac": v["valu_busy_frac"], "lane_util": v["lane_util"],
+            "valu_insts_per_segment": v["valu_insts_per_segment"],
+            "f64_tflops": round(flops / (k_ms * 1e-3) / 1e12, 3), "f64_peak_tflops": FP64_PEAK_TFLOPS,
+            "f64_frac": round(flops / (k_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS, 4), "source": v["source"]}
 
 
 def main():
@@ -81,9 +146,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and world > n_dev:
+        raise SystemExit(f"bench.py: {world} ranks but {n_dev} visible GPUs: one rank per GPU (RCCL refuses "
+                         "two ranks on one device); use --dist-backend gloo only to rehearse")
+    rehearsal = world > n_dev
     # --dist-backend gloo + fewer GPUs than ranks: a rehearsal of the multi-rank path on one box
     # (ranks share GPUs round-robin); the measured configuration is nccl (RCCL over xGMI)
-    local = local % max(1, torch.cuda.device_count())
+    local = local % max(1, n_dev)
     torch.cuda.set_device(local)
     if world > 1:
         if args.dist_backend == "nccl":
@@ -147,6 +217,7 @@ def main():
     k_ms = float(np.mean(kernel_ms))
     seg = float(np.mean(segments))
     achieved = BYTES_PER_SEGMENT * seg / (k_ms * 1e-3) / 1e9
+    achieved_f64 = BYTES_PER_SEGMENT_F64 * seg / (k_ms * 1e-3) / 1e9
     traffic = None
     tfile = os.path.join(REPO, "profiles", "traffic.json")
     if world == 1 and os.path.exists(tfile):  # (measured per N=1 launch; a rank's launch is smaller)
@@ -158,12 +229,13 @@ def main():
             traffic = None
     line = {
         "metric": "Msamples/sec (whole node) on book-1 random_scene 1200x800 @ 500spp; 1/2/4/8 GPU",
-        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 3), "unit": "Msamples/s", "n_gpus": min(world, n_dev), "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"{args.scene} {W}x{H} @ {args.spp}spp, max_depth {args.max_depth}, seed "
                                f"{args.seed:#x}", "scene": args.scene, "width": W, "height": H, "spp": args.spp,
                    "max_depth": args.max_depth, "bvh": args.bvh, "parallelism": f"tiles8x8/{world}",
+                   "ranks": world, "rehearsal": f"gloo, {world} ranks on {n_dev} GPU(s)" if rehearsal else None,
                    "engine": {1: "megakernel", 2: "wavefront"}.get(laps[-1][0]), "rounds": laps[-1][1],
                    "slots": laps[-1][2],
                    "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
@@ -174,7 +246,11 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),
-                     "bytes_per_segment": BYTES_PER_SEGMENT, "segments_per_launch": int(seg)},
+                     "bytes_per_segment": BYTES_PER_SEGMENT, "segments_per_launch": int(seg),
+                     "f64_state": {"bytes_per_segment": BYTES_PER_SEGMENT_F64, "achieved": round(achieved_f64, 2),
+                                   "frac": round(achieved_f64 / HBM_PEAK_GBS, 5)},
+                     "measured_hbm_gbs": round(traffic / (k_ms * 1e-3) / 1e9, 2) if traffic else None,
+                     "valu": valu_block(seg, k_ms, W, H, args) if world == 1 else None},
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu:

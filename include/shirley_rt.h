@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -176,6 +176,10 @@ typedef struct rt_scene_stats {
   int32_t n_leaves;
   int32_t depth;        /* max root-to-leaf depth */
   int64_t device_bytes; /* scene bytes resident in HBM */
+  /* ABI 4: the renderer's collapsed tree (the one rt_render* and RT_TRAVERSAL_RENDER walk) */
+  int32_t n_nodes4;     /* 4-wide f32 nodes */
+  int32_t wide_block;   /* 1: the trace kernel keeps the whole 4-wide tree in LDS (1024-thread blocks) */
+  double origin_limit;  /* rays with max|origin| above this take the f64 re-test of the f32 node boxes */
 } rt_scene_stats;
 
 /* Counters of the last render call (deterministic for a given seed). */
@@ -192,6 +196,9 @@ typedef struct rt_counters {
   double extend_ms;     /* wavefront + RT_ENGINE_TIMING: summed device time of wf_extend launches */
   double shade_ms;      /* ... wf_shade launches */
   double texture_ms;    /* ... wf_texture launches */
+  int32_t sample_chunk; /* ABI 4: samples per work unit the call used (auto-sized when params.sample_chunk == 0;
+                         * < samples means each pixel's sum is added up per chunk, then chunk sums in order) */
+  int32_t n_chunks;     /* ceil(samples / sample_chunk) */
 } rt_counters;
 
 typedef struct rt_ctx rt_ctx;
@@ -244,6 +251,16 @@ typedef struct rt_hit {
   double u, v;
 } rt_hit;
 int rt_scene_hit(rt_ctx* ctx, const double* rays, int32_t n, double t_min, double t_max, rt_hit* out);
+
+/* ABI 4: the same query through a chosen traversal.
+ *   RT_TRAVERSAL_BINARY: the 2-wide f64 tree (the reference's BboxTree as built; what rt_scene_hit walks);
+ *   RT_TRAVERSAL_RENDER: the traversal the trace kernel runs — the 4-wide collapsed tree with conservative
+ *     f32 (inflated) child boxes, exact f64 leaf re-tests and an f64 fallback for rays whose origin lies
+ *     beyond rt_scene_stats.origin_limit, with nodes and primitives read from where the renderer reads them.
+ * Both return the reference's closest hit (bbox_tree.rs:56-91 + hit2 + the object tests). */
+enum { RT_TRAVERSAL_BINARY = 0, RT_TRAVERSAL_RENDER = 1 };
+int rt_scene_hit_ex(rt_ctx* ctx, const double* rays, int32_t n, double t_min, double t_max, int32_t traversal,
+                    rt_hit* out);
 
 /* Counters (segments etc.) of the most recent render call; blocks until it finished. */
 int rt_counters_get(rt_ctx* ctx, rt_counters* out);

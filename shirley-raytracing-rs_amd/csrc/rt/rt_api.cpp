@@ -32,6 +32,8 @@ hipError_t launch_unpack(const double* gathered, int world, int max_tiles, int n
                          int height, double* out, hipStream_t stream);
 hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, double t_max, void* out,
                       hipStream_t stream);
+hipError_t launch_hit4(const DScene& S, bool wide, const double* rays, int n, double t_min, double t_max, void* out,
+                       hipStream_t stream);
 // wavefront.hip
 size_t wf_extend_lds(int n_lds_nodes, int stack_depth);
 int wf_extend_threads();
@@ -79,7 +81,7 @@ struct rt_ctx {
   hipEvent_t wf_ev[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> lap_ev;    // RT_ENGINE_TIMING: one event after every launch
   bool have_timing = false;
-  int last_engine = 0, last_iters = 0, last_timing = 0;
+  int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0;
   uint64_t last_slots = 0;
   double lap_ms[3] = {0, 0, 0};
 };
@@ -757,6 +759,8 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
   HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
   c->last_engine = engine;
+  c->last_chunk = chunk;
+  c->last_n_chunks = n_chunks;
   c->last_iters = 0;
   c->last_slots = 0;
   c->last_timing = 0;
@@ -1042,6 +1046,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   for (const auto& n : tree.nodes) leaves += n.leaf >= 0;
   c->stats.n_leaves = leaves;
   c->stats.depth = depth;
+  c->stats.n_nodes4 = S.n_nodes4;
+  c->stats.wide_block = c->mk_threads == kTraceThreadsWide ? 1 : 0;
+  c->stats.origin_limit = S.origin_limit;
   c->stats.device_bytes = (int64_t)(nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim) +
                                     mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex) +
                                     perl.size() * sizeof(DPerlin) + imgs.size() * sizeof(DImage) + texels.size());
@@ -1122,9 +1129,16 @@ int rt_render_scanlines(rt_ctx* c, const rt_camera* cam, const rt_render_params*
 }
 
 int rt_scene_hit(rt_ctx* c, const double* rays, int32_t n, double t_min, double t_max, rt_hit* out) {
+  return rt_scene_hit_ex(c, rays, n, t_min, t_max, RT_TRAVERSAL_BINARY, out);
+}
+
+int rt_scene_hit_ex(rt_ctx* c, const double* rays, int32_t n, double t_min, double t_max, int32_t traversal,
+                    rt_hit* out) {
   if (!c) return RT_E_INVALID;
   if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded");
   if (n < 0 || (n > 0 && (!rays || !out))) return fail(c, RT_E_INVALID, "bad ray batch");
+  if (traversal != RT_TRAVERSAL_BINARY && traversal != RT_TRAVERSAL_RENDER)
+    return fail(c, RT_E_INVALID, "bad traversal %d", traversal);
   if (n == 0) return RT_OK;
   static_assert(sizeof(rt_hit) == 80, "rt_hit layout");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -1132,7 +1146,10 @@ int rt_scene_hit(rt_ctx* c, const double* rays, int32_t n, double t_min, double 
   int st = upload(c, r, rays, (size_t)n * 6 * sizeof(double));
   if (!st) st = ensure(c, h, (size_t)n * sizeof(rt_hit));
   if (!st) {
-    hipError_t e = launch_hit(c->scene, static_cast<const double*>(r.p), n, t_min, t_max, h.p, c->stream);
+    const double* rd = static_cast<const double*>(r.p);
+    hipError_t e = traversal == RT_TRAVERSAL_RENDER
+                       ? launch_hit4(c->scene, c->mk_threads == kTraceThreadsWide, rd, n, t_min, t_max, h.p, c->stream)
+                       : launch_hit(c->scene, rd, n, t_min, t_max, h.p, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(out, h.p, (size_t)n * sizeof(rt_hit), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) st = fail(c, RT_E_HIP, "rt_scene_hit: %s", hipGetErrorString(e));
@@ -1187,6 +1204,8 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
   out->kernel_ms = a;
   out->reduce_ms = b;
   out->engine = c->last_engine;
+  out->sample_chunk = c->last_chunk;
+  out->n_chunks = c->last_n_chunks;
   out->iterations = c->last_iters;
   out->slots = c->last_slots;
   if (c->last_timing) {

@@ -158,9 +158,10 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
       if (!active) sum = sum + em;  // max_depth == 0: ray_color returns black (render.rs:30)
     }
     if (!__any(active)) {
-      if (exhausted || __ballot(has_unit) == 0ull) {
-        if (exhausted) break;
-      }
+      // done only when the pool is drained AND no lane still holds a unit: with max_depth == 0 a
+      // lane's samples never become active, so its unit advances (and publishes) in these
+      // iterations alone
+      if (exhausted && __ballot(has_unit) == 0ull) break;
       continue;
     }
     // 4. one ray_color iteration (render.rs:30-46): closest hit, then emitted + scatter or sky
@@ -390,6 +391,56 @@ __global__ __launch_bounds__(kHitThreads) void hit_kernel(DScene S, const double
   out[i] = r;
 }
 
+// Closest hit for a batch of rays through the traversal the renderer runs (rt_scene_hit_ex with
+// RT_TRAVERSAL_RENDER): the 4-wide tree with conservative f32 (inflated) child boxes, exact f64 leaf
+// re-tests and the f64 fallback for far origins (traverse4), with nodes / primitives read from the
+// place trace_kernel reads them (MODE) and the trace kernel's EXT instance.  One lane per ray; the
+// hit record is rebuilt like hit_kernel's.
+template <int MODE, bool EXT>
+__global__ __launch_bounds__(kHitThreads) void hit4_kernel(DScene S, const double* __restrict__ rays, int n,
+                                                           double t_min, double t_max, HitOut* __restrict__ out) {
+  extern __shared__ unsigned char lds_raw[];
+  const int tid = threadIdx.x;
+  DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)S.n_lds_nodes4 * sizeof(DNode4F));
+  unsigned char* stk_base = lds_raw + (size_t)S.n_lds_nodes4 * sizeof(DNode4F) +
+                            (MODE == kSceneLds ? (size_t)S.n_lds_prims * sizeof(DPrim) +
+                                                     (size_t)S.n_lds_perlin * sizeof(DPerlin)
+                                               : 0);
+  unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;
+  stage_nodes4<MODE>(S, lds_nodes, lds_prims);
+  const int i = blockIdx.x * kHitThreads + tid;
+  if (i >= n) return;
+  const v3 o = V(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
+  const v3 d = V(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
+  double t_best = t_max;
+  int face = -1;
+  unsigned visits = 0, ptests = 0;
+  const Rng rk{(uint32_t)i, 0u, 0u, 0u, 0u};  // side-stream key of a free ray, as hit_kernel's
+#ifdef RT_PHASE_TIMING
+  unsigned long long steps = 0;
+  const int prim = traverse4<kHitThreads, MODE, EXT>(S, lds_nodes, lds_prims, o, d, t_min, t_best, face, stk, rk, 0ull,
+                                                      visits, ptests, steps);
+#else
+  const int prim = traverse4<kHitThreads, MODE, EXT>(S, lds_nodes, lds_prims, o, d, t_min, t_best, face, stk, rk, 0ull,
+                                                      visits, ptests);
+#endif
+  HitOut r{};
+  r.object = prim;
+  if (prim >= 0) {
+    const DPrim pr = S.prims[prim];
+    Hit h;
+    hit_record<true, true>(S, pr, face, o, d, t_best, rk, 0ull, h);
+    r.front_face = h.front_face ? 1 : 0;
+    r.t = h.t;
+    r.point[0] = h.point.x; r.point[1] = h.point.y; r.point[2] = h.point.z;
+    r.normal[0] = h.normal.x; r.normal[1] = h.normal.y; r.normal[2] = h.normal.z;
+    r.u = h.u;
+    r.v = h.v;
+  }
+  out[i] = r;
+}
+
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
@@ -485,6 +536,42 @@ hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, 
     default: hipLaunchKernelGGL(hit_kernel<kNodesMixed>, dim3(blocks), dim3(kHitThreads), lds, stream, S, rays, n, t_min, t_max, o);
   }
   return hipGetLastError();
+}
+
+template <int MODE, bool EXT>
+static hipError_t launch_hit4_1(const DScene& S, const double* rays, int n, double t_min, double t_max, HitOut* o,
+                                int blocks, hipStream_t stream) {
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, MODE == kSceneLds ? S.n_lds_prims : 0,
+                                     MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads);
+  hipError_t e = hipFuncSetAttribute((const void*)hit4_kernel<MODE, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((hit4_kernel<MODE, EXT>), dim3(blocks), dim3(kHitThreads), lds, stream, S, rays, n, t_min, t_max, o);
+  return hipGetLastError();
+}
+template <int MODE>
+static hipError_t launch_hit4_m(const DScene& S, const double* rays, int n, double t_min, double t_max, HitOut* o,
+                                int blocks, hipStream_t stream) {
+  return S.exts ? launch_hit4_1<MODE, true>(S, rays, n, t_min, t_max, o, blocks, stream)
+                : launch_hit4_1<MODE, false>(S, rays, n, t_min, t_max, o, blocks, stream);
+}
+
+// rt_scene_hit_ex(RT_TRAVERSAL_RENDER): the node / primitive placement the trace kernel uses
+// (`wide`: the scene-in-LDS block of launch_trace).
+hipError_t launch_hit4(const DScene& S, bool wide, const double* rays, int n, double t_min, double t_max, void* out,
+                       hipStream_t stream) {
+  const int blocks = (n + kHitThreads - 1) / kHitThreads;
+  if (blocks == 0) return hipSuccess;
+  HitOut* o = static_cast<HitOut*>(out);
+  if (wide) {
+    if (S.n_lds_prims > 0) return launch_hit4_m<kSceneLds>(S, rays, n, t_min, t_max, o, blocks, stream);
+    return launch_hit4_m<kNodesLds>(S, rays, n, t_min, t_max, o, blocks, stream);
+  }
+  switch (node_mode4(S)) {
+    case kNodesLds: return launch_hit4_m<kNodesLds>(S, rays, n, t_min, t_max, o, blocks, stream);
+    case kNodesGlobal: return launch_hit4_m<kNodesGlobal>(S, rays, n, t_min, t_max, o, blocks, stream);
+    default: return launch_hit4_m<kNodesMixed>(S, rays, n, t_min, t_max, o, blocks, stream);
+  }
 }
 
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,

@@ -23,6 +23,7 @@ RT_SKY_ABOVE, RT_SKY_FLAT, RT_SKY_NONE = range(3)
 RT_BVH_REFERENCE, RT_BVH_SAH = 0, 1
 RT_BVH_NODES_GLOBAL, RT_BVH_NODES_HALF_LDS, RT_BVH_NODES_LDS = 0x100, 0x200, 0x400
 RT_ENGINE_AUTO, RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_TIMING = 0, 1, 2, 0x10
+RT_TRAVERSAL_BINARY, RT_TRAVERSAL_RENDER = 0, 1
 
 _d3 = C.c_double * 3
 _d6 = C.c_double * 6
@@ -77,14 +78,18 @@ class rt_render_params(C.Structure):
 
 class rt_scene_stats(C.Structure):
     _fields_ = [("n_objects", C.c_int32), ("n_nodes", C.c_int32), ("n_leaves", C.c_int32),
-                ("depth", C.c_int32), ("device_bytes", C.c_int64)]
+                ("depth", C.c_int32), ("device_bytes", C.c_int64),
+                # ABI 4
+                ("n_nodes4", C.c_int32), ("wide_block", C.c_int32), ("origin_limit", C.c_double)]
 
 
 class rt_counters(C.Structure):
     _fields_ = [("samples", C.c_uint64), ("segments", C.c_uint64), ("node_visits", C.c_uint64),
                 ("prim_tests", C.c_uint64), ("kernel_ms", C.c_double), ("reduce_ms", C.c_double),
                 ("engine", C.c_int32), ("iterations", C.c_int32), ("slots", C.c_uint64),
-                ("extend_ms", C.c_double), ("shade_ms", C.c_double), ("texture_ms", C.c_double)]
+                ("extend_ms", C.c_double), ("shade_ms", C.c_double), ("texture_ms", C.c_double),
+                # ABI 4
+                ("sample_chunk", C.c_int32), ("n_chunks", C.c_int32)]
 
 
 class rt_bvh_node(C.Structure):
@@ -124,6 +129,8 @@ RT_SIGNATURES = {
     "rt_unpack_tiles_device": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.c_int32, C.c_void_p, C.c_void_p,
                                          C.c_void_p]),
     "rt_scene_hit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.POINTER(rt_hit)]),
+    "rt_scene_hit_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_int32,
+                                  C.POINTER(rt_hit)]),
     "rt_synchronize": (C.c_int, [C.c_void_p]),
     "rt_counters_get": (C.c_int, [C.c_void_p, C.POINTER(rt_counters)]),
     "rt_bvh_build_host": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int32, C.POINTER(C.c_int32),

@@ -115,11 +115,18 @@ class Device:
         _check(self._h, N.rt_lib().rt_tonemap_device(self._h, C.c_void_p(accum_ptr), int(width), int(height),
                                                      int(samples), C.c_void_p(rgb8_ptr), C.c_void_p(stream or None)))
 
-    def hit(self, rays: np.ndarray, t_min: float = 0.001, t_max: float = float("inf")):
-        """Closest hits for rays [n][6] (Hittable for Scene, scene/mod.rs:180-190) -> rt_hit array."""
+    def hit(self, rays: np.ndarray, t_min: float = 0.001, t_max: float = float("inf"), traversal: str = "binary"):
+        """Closest hits for rays [n][6] (Hittable for Scene, scene/mod.rs:180-190) -> rt_hit array.
+        traversal: "binary" (the 2-wide f64 tree, rt_scene_hit) or "render" (the 4-wide f32-inflated
+        traversal the trace kernel runs, rt_scene_hit_ex(RT_TRAVERSAL_RENDER))."""
         r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
         out = (N.rt_hit * max(1, len(r)))()
-        _check(self._h, N.rt_lib().rt_scene_hit(self._h, r.ctypes.data, len(r), float(t_min), float(t_max), out))
+        if traversal == "binary":
+            code = N.rt_lib().rt_scene_hit(self._h, r.ctypes.data, len(r), float(t_min), float(t_max), out)
+        else:
+            tv = {"render": N.RT_TRAVERSAL_RENDER}[traversal]
+            code = N.rt_lib().rt_scene_hit_ex(self._h, r.ctypes.data, len(r), float(t_min), float(t_max), tv, out)
+        _check(self._h, code)
         return out[:len(r)]
 
     def synchronize(self):

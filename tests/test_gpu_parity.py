@@ -6,7 +6,11 @@ so per-sample colours agree to the last ulp except where the device's transcende
 acos, atan2, pow) differ from glibc's by an ulp — a last-bit difference in an attenuation — or,
 rarely, such an ulp flips a comparison (checker sign, Schlick vs U, texel index) or two objects tie
 at exactly the same t, which changes one whole path.  The test therefore demands
-  * >= 95 % of pixel channels bit-identical (sample_chunk = spp: in-order sums like render.rs:58-69),
+  * >= 99 % of pixel channels bit-identical (sample_chunk = spp: in-order sums like render.rs:58-69),
+    and per scene no fewer than measured on MI355X minus a small margin (EXACT_MIN: scenes without
+    the Perlin marble's sin are bit-identical on every channel measured; round-2 calibration in
+    gpurun_out/parity_fractions.jsonl: random 0.9967, perlin 0.9949, box-light 0.9985, final:6:60
+    0.9994, 1200-wide rows 0.9915, every other scene 1.0),
   * every channel within TOL = 1e-10 * spp absolute of the oracle, except at most 0.1 % of pixels
     (a flipped path changes one sample by up to the path's radiance).
 Both trace engines (RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT) run the same binary64 code on the same
@@ -26,12 +30,24 @@ SEED = 0x5EED
 ENGINES = ["megakernel", "wavefront"]
 
 
-def check_parity(gpu_img, ora_img, spp, frac_exact=0.95, frac_outlier=0.001):
+def _log_fraction(exact, bad, shape):
+    """SHIRLEY_PARITY_LOG=<file>: append each comparison's measured fractions (threshold calibration)."""
+    import json
+    import os
+    path = os.environ.get("SHIRLEY_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": os.environ.get("PYTEST_CURRENT_TEST", "?"), "exact": float(exact),
+                                "bad_px": float(bad), "shape": list(shape)}) + "\n")
+
+
+def check_parity(gpu_img, ora_img, spp, frac_exact=0.99, frac_outlier=0.001):
     assert gpu_img.shape == ora_img.shape
     assert np.isfinite(gpu_img).all() == np.isfinite(ora_img).all()
     exact = np.mean(gpu_img == ora_img)
     diff = np.abs(gpu_img - ora_img)
     bad_px = np.any(diff > 1e-10 * spp, axis=-1)
+    _log_fraction(exact, bad_px.mean(), gpu_img.shape)
     assert exact >= frac_exact, f"only {exact:.5f} of channels bit-identical (max diff {diff.max():.3g})"
     assert bad_px.mean() <= frac_outlier, f"{bad_px.sum()} pixels outside tolerance"
 
@@ -42,6 +58,11 @@ SCENES = [("random", 48, "std16x9"), ("random-night", 48, "std16x9"), ("demo", 4
           # book-2 extensions (absent from the reference; oracle restatement, parity unpinned):
           # reduced final scene (whole scene in LDS) and the full one (1409 objects, tree via L1/L2)
           ("final:6:60", 40, "square"), ("final", 32, "square")]
+
+
+# fraction of bit-identical channels required per scene (measured - margin; see the module docstring)
+EXACT_MIN = {"random": 0.995, "random-night": 0.9995, "demo": 0.9995, "perlin": 0.993, "earth": 0.9995,
+             "box-light": 0.997, "cornell": 0.9995, "final:6:60": 0.998, "final": 0.9995}
 
 
 @pytest.mark.parametrize("name,width,aspect", SCENES)
@@ -55,7 +76,7 @@ def test_render_matches_oracle(gpu, name, width, aspect):
     for engine in ENGINES:
         img = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp,
                                                 engine=engine))
-        check_parity(img, ora, spp)
+        check_parity(img, ora, spp, frac_exact=EXACT_MIN[name])
         cnt = gpu.counters()
         assert cnt.engine == {"megakernel": 1, "wavefront": 2}[engine]
         assert cnt.samples == cam.image_width * cam.image_height * spp == ocnt.samples
@@ -75,7 +96,7 @@ def test_render_matches_golden(gpu, name, aspect):
     gpu.upload(rt.SceneBuilder.builtin(name, SEED).finalize(SEED))
     img = gpu.render(rt.scene_camera(name, 32, aspect), rt.RenderSettings(samples=8, max_reflect=50, seed=SEED,
                                                                           sample_chunk=8))
-    check_parity(img, gold[key], 8)
+    check_parity(img, gold[key], 8, frac_exact=EXACT_MIN.get(name, 0.999))
 
 
 def test_hit_queries_match_golden(gpu):
@@ -270,7 +291,7 @@ def test_scanlines_equal_full_frame(gpu, engine):
     osc = O.OracleScene(scene)
     O.lib().or_render_scanline(osc.h, C.byref(cam), C.byref(O.params(spp, 50, SEED)), 9, row.ctypes.data,
                                C.byref(cnt))
-    check_parity(part[4:5], row[None], spp, frac_exact=0.9, frac_outlier=0.05)
+    check_parity(part[4:5], row[None], spp, frac_exact=0.99, frac_outlier=0.05)
 
 
 @pytest.mark.parametrize("engine", ENGINES)
@@ -399,3 +420,92 @@ def test_cli_render_device_output_stage(tmp_path):
     assert np.array_equal(img_a, img_b)
     sums = np.fromfile(acc, dtype=np.float64).reshape(img_a.shape[0], img_a.shape[1], 3)
     assert np.array_equal(rt.to_image(sums, 4), img_a)
+
+
+def test_headline_settings_band_matches_oracle(gpu):
+    """BASELINE config 2 exactly as bench.py runs it: 1200x800 @ 500 spp, max_depth 50, SAH tree,
+    rt_render_device with sample_chunk = 0 (auto: several chunks per pixel, so each pixel's sum is
+    added per chunk and the chunk sums in order — not render.rs:58-69's one running sum).  A 16-row
+    band of that frame against (1) the GPU's in-order sums of the same samples: only the addition order
+    differs, every channel within 1e-12 relative (500 non-negative terms: <= 499 ulp-level roundings);
+    (2) the oracle's in-order render: the stated parity tolerance, with the exact-bit gate."""
+    import torch
+    spp, r0, r1 = 500, 392, 408
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    cam = rt.default_camera(1200, "std3x2")
+    gpu.upload(scene, "sah")
+    accum = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.float64, device="cuda")
+    gpu.render_device(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED), accum.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    c = gpu.counters()
+    assert 1 < c.sample_chunk < spp and c.n_chunks == -(-spp // c.sample_chunk) > 1
+    band = accum[r0:r1].cpu().numpy()
+    inorder = gpu.render_scanlines(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp),
+                                   r0, r1)
+    assert gpu.counters().n_chunks == 1
+    assert np.all(np.abs(band - inorder) <= 1e-12 * np.abs(inorder))
+    ora, cnt = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), r0, r1, threads=16)
+    assert cnt.samples == 1200 * (r1 - r0) * spp
+    check_parity(inorder, ora, spp, frac_exact=0.99)
+    # the bench frame's own band: reordering tolerance, plus the flipped-path allowance of check_parity
+    bad = np.any(np.abs(band - ora) > 1e-12 * np.abs(ora) + 1e-10 * spp * (band != inorder), axis=-1)
+    assert bad.mean() <= 0.001
+
+
+def test_max_depth_zero_partial_units(gpu):
+    """max_depth 0 (ray_color's loop never runs: black, render.rs:30) with units that end at different
+    iterations: a width that is not a multiple of 8 (edge tiles with idle lanes), and a sample chunk
+    shorter than spp with a short last chunk — every unit must still publish (all-zero image, no stale
+    partial sums)."""
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    gpu.upload(scene)
+    cam = rt.default_camera(37, "std16x9")
+    # leave garbage in the partial buffer first
+    gpu.render(cam, rt.RenderSettings(samples=7, seed=SEED, sample_chunk=3))
+    for engine in ENGINES:
+        for chunk in (0, 1, 3, 7):
+            img = gpu.render(cam, rt.RenderSettings(engine=engine, samples=7, max_reflect=0, seed=SEED,
+                                                    sample_chunk=chunk))
+            assert not img.any(), (engine, chunk)
+            assert gpu.counters().samples == cam.image_width * cam.image_height * 7
+
+
+def test_final_scene_tile_sharded_world8(gpu):
+    """BASELINE config 5's data path on one device: book-2 final_scene (1409 objects, EXT kernels,
+    tree via L1/L2) rendered as the 8 ranks' interleaved tiles (rt_render_tiles_device), gathered
+    rank-major and scattered back (rt_unpack_tiles_device): bit-identical to the full frame."""
+    import torch
+    spp, world = 3, 8
+    scene = rt.scenes.final_scene(SEED).finalize(SEED)
+    cam = rt.scene_camera("final", 61, "square")  # 61 x 61: partial edge tiles
+    gpu.upload(scene)
+    full = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
+    n_total, max_tiles = rt.tile_layout(cam, world)
+    assert n_total == 64 and max_tiles == 8
+    gathered = torch.zeros((world, max_tiles, 64, 3), dtype=torch.float64, device="cuda")
+    for r in range(world):
+        gpu.render_tiles_device(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp, tile_rank=r,
+                                                       tile_world=world), gathered[r].data_ptr())
+    gpu.synchronize()
+    accum = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.float64, device="cuda")
+    gpu.unpack_tiles_device(cam, world, gathered.data_ptr(), accum.data_ptr())
+    gpu.synchronize()
+    assert np.array_equal(accum.cpu().numpy(), full)
+    ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
+    check_parity(full, ora, spp)
+
+
+@pytest.mark.parametrize("bvh", ["reference", "sah"])
+def test_gen_spheres_side11_matches_oracle(gpu, bvh):
+    """The config-5 stand-in at full scale: gen_spheres side 11 = 22^3 = 10,648 spheres
+    (benches/my_benchmark.rs:35-60), tree through L1/L2 (too large for LDS), both builders."""
+    spp = 2
+    scene = rt.scenes.gen_spheres(0xDEADBEEF, 11).finalize(1)
+    assert scene.desc.n_objects == 10648
+    cam = rt.scene_camera("spheres", 48, "std16x9")
+    gpu.upload(scene, bvh)
+    assert gpu.stats().wide_block == 0
+    img = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
+    ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
+    check_parity(img, ora, spp, frac_exact=0.9995)
