@@ -3,10 +3,10 @@
 (BASELINE.json configs[1]; metric "Msamples/sec (whole node)").
 
 One step = one full frame through the hot path (camera rays -> ray_color bounce loop -> per-pixel
-sums in HBM).  N GPUs (torchrun, one process per GPU, RCCL): the frame's 8x8 tiles are dealt
-round-robin to ranks, each rank renders its tiles into a packed buffer and rank 0 gathers them over
-xGMI (the north star's exchange step) and scatters them into the [H][W][3] image: strong scaling of
-one frame.  Scene upload happens before the timed region; inputs are resident in HBM.
+sums in HBM).  N GPUs (torchrun, one process per GPU): the frame's 8x8 tiles are dealt round-robin to
+ranks; each rank calls rt_render_sharded (C ABI), which renders its tiles into a packed buffer and
+gathers them to rank 0 with RCCL (ncclGather over xGMI, the north star's exchange step), where they
+are scattered into the [H][W][3] image: strong scaling of one frame.  Scene upload happens before the timed region; inputs are resident in HBM.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` (dominant kernel:
 the persistent trace kernel, timed with HIP events on the launch stream) and `cpu_baseline` (the f64
@@ -172,17 +172,27 @@ def main():
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+    comm = None
     if world > 1:
         n_tiles, max_tiles = rt.tile_layout(cam, world)
-        packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
-        from raytracer.parallel import gather_tiles
+        if args.dist_backend == "nccl":
+            # the tile gather runs behind the C ABI (rt_render_sharded: ncclGather to rank 0 over xGMI);
+            # torch.distributed only carries the communicator id, the barriers and the max-over-ranks clock
+            uid = [rt.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            comm = dev.comm_init_rank(uid[0], world, rank)
+        else:
+            packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
+            from raytracer.parallel import gather_tiles
 
     def step():
         if world == 1:
             dev.render_device(cam, settings, accum.data_ptr(), sh)
-        else:
+        elif comm is not None:
+            dev.render_sharded(comm, cam, settings, accum.data_ptr() if rank == 0 else 0, sh)
+        else:  # gloo rehearsal (ranks sharing one GPU cannot form an RCCL communicator)
             dev.render_tiles_device(cam, settings, packed.data_ptr(), sh)
-            gathered = gather_tiles(packed, world)  # RCCL all-gather over xGMI; rank 0 assembles the frame
+            gathered = gather_tiles(packed, world)
             if rank == 0:
                 dev.unpack_tiles_device(cam, world, gathered.data_ptr(), accum.data_ptr(), sh)
 
@@ -257,6 +267,8 @@ def main():
         line["cpu_baseline"] = cpu_baseline(scene, cam, args)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     dev.close()
     if world > 1:
         dist.destroy_process_group()

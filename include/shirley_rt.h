@@ -34,7 +34,8 @@ typedef enum rt_status {
   RT_E_INVALID = 1,     /* bad argument / malformed scene */
   RT_E_HIP = 2,         /* HIP runtime error (no device, launch failure, ...) */
   RT_E_OOM = 3,         /* device allocation failed */
-  RT_E_UNSUPPORTED = 4  /* feature not compiled in / not available */
+  RT_E_UNSUPPORTED = 4, /* feature not compiled in / not available */
+  RT_E_RCCL = 5         /* RCCL (librccl) missing or a collective failed (multi-GPU entry points) */
 } rt_status;
 
 /* geometry/object.rs:9-16  GeometricObject */
@@ -261,6 +262,34 @@ int rt_scene_hit(rt_ctx* ctx, const double* rays, int32_t n, double t_min, doubl
 enum { RT_TRAVERSAL_BINARY = 0, RT_TRAVERSAL_RENDER = 1 };
 int rt_scene_hit_ex(rt_ctx* ctx, const double* rays, int32_t n, double t_min, double t_max, int32_t traversal,
                     rt_hit* out);
+
+/* ---- multi-GPU (ABI 4) -------------------------------------------------------
+ * The frame's 8x8 tiles are dealt round-robin over the ranks of a communicator (tile k -> rank
+ * k % world); each rank renders its tiles into a packed buffer and RCCL gathers the packed buffers to
+ * rank 0 over xGMI (ncclGather), which scatters them into the [H][W][3] image.  The counter RNG is
+ * keyed by the global pixel, so the frame is bit-identical for every world size.  Replaces the
+ * reference's whole-machine rayon loop over scanlines (main.rs:92-126).  RCCL is loaded on first use
+ * (dlopen "librccl.so.1": the copy already in the process if any); without it these calls return
+ * RT_E_RCCL.
+ *
+ * One process per GPU: rank 0 calls rt_comm_unique_id, hands the id to every rank by any channel
+ * (torch.distributed's store, MPI, a file), and each rank calls rt_comm_init_rank on its own ctx.
+ * One process driving several GPUs: rt_render_multi (communicators created and cached per ctx set). */
+#define RT_COMM_ID_BYTES 128
+typedef struct rt_comm rt_comm;
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+int rt_comm_init_rank(rt_ctx* ctx, const uint8_t id[RT_COMM_ID_BYTES], int32_t world, int32_t rank, rt_comm** out);
+int rt_comm_destroy(rt_comm* comm);
+/* One rank's share of a sharded frame, asynchronous on `stream` (NULL: the ctx's stream): render the
+ * rank's tiles (params->tile_rank / tile_world are ignored: the communicator's rank and size are used),
+ * gather to rank 0, and on rank 0 scatter into accum_dev ([H][W][3] f64 sums on its device; NULL on the
+ * other ranks).  Every rank of the communicator must make the call (a collective). */
+int rt_render_sharded(rt_ctx* ctx, rt_comm* comm, const rt_camera* cam, const rt_render_params* params,
+                      double* accum_dev, void* stream);
+/* The whole frame on n devices from one process, blocking; accum_host as rt_render's ([H][W][3] sums, row
+ * 0 = bottom).  ctxs[0] is the root; every ctx needs the same scene uploaded.  n == 1 equals rt_render. */
+int rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_camera* cam, const rt_render_params* params,
+                    double* accum_host);
 
 /* Counters (segments etc.) of the most recent render call; blocks until it finished. */
 int rt_counters_get(rt_ctx* ctx, rt_counters* out);

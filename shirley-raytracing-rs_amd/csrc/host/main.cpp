@@ -9,7 +9,9 @@
 // --camera-focal-length 1.0, --camera-aperture 0.001, --camera-aspect-ratio std3x2;
 // random: --night, --scene-output FILE; saved: <scene_input>.
 // Added: --seed N (the reference is unseeded), --device N, --bvh reference|sah, --sample-chunk N,
-// --dump-accum FILE (raw f64 [H][W][3] sums, row 0 = bottom), --side-len N (spheres).
+// --dump-accum FILE (raw f64 [H][W][3] sums, row 0 = bottom), --side-len N (spheres),
+// --gpus N (devices [device, device + N): the frame's tiles sharded over N GPUs with an RCCL gather,
+// rt_render_multi — the counterpart of the reference's whole-machine rayon loop, main.rs:117-125).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -30,7 +32,7 @@ int verbose = 0;
 
 struct Args {
   std::string scene, output = "out.png", scene_output, scene_input, dump_accum, aspect = "std3x2", bvh = "reference";
-  int samples = 100, max_reflect = 50, width = 640, device = 0, sample_chunk = 0, side_len = 11;
+  int samples = 100, max_reflect = 50, width = 640, device = 0, sample_chunk = 0, side_len = 11, gpus = 1;
   double fov = 20.0, focal = 1.0, aperture = 0.001;
   bool night = false, single_threaded = false;
   unsigned long long seed = 0x5EED;
@@ -44,8 +46,60 @@ struct Args {
                "options: -o FILE -s N -m N -w N --single-threaded --camera-fov F --camera-focal-length F\n"
                "         --camera-aperture F --camera-aspect-ratio std3x2|std16x9|std16x10|square|target-iphone\n"
                "         --night --scene-output FILE (random)  <scene_input> (saved)  --side-len N (spheres)\n"
-               "         --seed N --device N --bvh reference|sah --sample-chunk N --dump-accum FILE\n");
+               "         --seed N --device N --gpus N --bvh reference|sah --sample-chunk N --dump-accum FILE\n");
   std::exit(2);
+}
+
+// --gpus N > 1: one ctx per device, the scene uploaded to each, rt_render_multi (tiles + RCCL gather
+// to the first device), to_image on the host.
+int render_scene_multi(const Args& a, const rt_scene_desc* desc, const rt_camera& cam, int samples) {
+  std::vector<rt_ctx*> ctxs(a.gpus, nullptr);
+  int st = 0;
+  auto done = [&](int rc) {
+    for (rt_ctx* c : ctxs)
+      if (c) rt_destroy(c);
+    return rc;
+  };
+  const int builder = a.bvh == "sah" ? RT_BVH_SAH : RT_BVH_REFERENCE;
+  for (int i = 0; i < a.gpus; ++i) {
+    if ((st = rt_create(a.device + i, &ctxs[i]))) {
+      std::fprintf(stderr, "error: rt_create(device %d) failed (%d)\n", a.device + i, st);
+      return done(1);
+    }
+    if ((st = rt_scene_upload(ctxs[i], desc, builder))) {
+      std::fprintf(stderr, "error: %s\n", rt_last_error(ctxs[i]));
+      return done(1);
+    }
+  }
+  rt_render_params p{};
+  p.samples = samples;
+  p.max_depth = a.max_reflect;
+  p.seed = a.seed;
+  p.tile_world = 1;
+  p.sample_chunk = a.sample_chunk;
+  const size_t n = (size_t)cam.image_width * cam.image_height * 3;
+  std::vector<double> accum(n);
+  std::vector<uint8_t> rgb(n);
+  auto t1 = std::chrono::steady_clock::now();
+  if ((st = rt_render_multi(ctxs.data(), a.gpus, &cam, &p, accum.data()))) {
+    std::fprintf(stderr, "error: %s\n", rt_last_error(ctxs[0]));
+    return done(1);
+  }
+  auto t2 = std::chrono::steady_clock::now();
+  const double ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+  if (verbose >= 1)
+    std::fprintf(stderr, "INFO %d GPUs: render %.1f ms (incl. gather and copy-back): %.1f Msamples/s\n", a.gpus, ms,
+                 (double)cam.image_width * cam.image_height * samples / (ms * 1e3));
+  rt_tonemap(accum.data(), cam.image_width, cam.image_height, samples, rgb.data());  // image.rs:31-44
+  if (!a.dump_accum.empty()) {
+    std::ofstream f(a.dump_accum, std::ios::binary);
+    f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
+  }
+  if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
+    std::fprintf(stderr, "error: %s\n", sh_last_error());
+    return done(1);
+  }
+  return done(0);
 }
 
 int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam) {
@@ -54,6 +108,7 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
     std::fprintf(stderr, "WARN samples set to 0, using 1\n");
     samples = 1;
   }
+  if (a.gpus > 1) return render_scene_multi(a, desc, cam, samples);
   rt_ctx* ctx = nullptr;
   int st = rt_create(a.device, &ctx);
   if (st) {
@@ -154,6 +209,7 @@ int main(int argc, char** argv) {
     else if (s == "--scene-output") a.scene_output = next();
     else if (s == "--seed") a.seed = std::strtoull(next().c_str(), nullptr, 0);
     else if (s == "--device") a.device = std::atoi(next().c_str());
+    else if (s == "--gpus") a.gpus = std::atoi(next().c_str());
     else if (s == "--bvh") a.bvh = next();
     else if (s == "--sample-chunk") a.sample_chunk = std::atoi(next().c_str());
     else if (s == "--dump-accum") a.dump_accum = next();
@@ -170,6 +226,7 @@ int main(int argc, char** argv) {
   if (pos[0] != "render" || pos.size() < 2) usage("expected `render <scene>`");
   a.scene = pos[1];
   if (a.samples < 0 || a.max_reflect < 0 || a.width < 1) usage("samples / max-reflect / width out of range");
+  if (a.gpus < 1 || a.gpus > 64) usage("--gpus must be in [1, 64]");
 
   sh_scene* scene = nullptr;
   std::string cam_scene = a.scene;

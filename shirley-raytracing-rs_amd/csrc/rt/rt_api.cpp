@@ -16,6 +16,7 @@
 
 #include "../../../include/shirley_rt.h"
 #include "bvh_build.h"
+#include "rccl_loader.h"
 #include "rt_layout.h"
 
 namespace rt {
@@ -54,6 +55,12 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
+// A rank of an RCCL communicator (multi-GPU frame sharding).
+struct rt_comm {
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0, device = 0;
+};
+
 struct rt_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -84,6 +91,11 @@ struct rt_ctx {
   int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0;
   uint64_t last_slots = 0;
   double lap_ms[3] = {0, 0, 0};
+  // multi-GPU: this rank's packed tiles, the root's gathered buffer, and (root of rt_render_multi)
+  // the communicators of the device set last used, kept for the next call
+  DevBuf packed, gathered;
+  std::vector<int> group_devices;
+  std::vector<rt_comm> group_comms;
 };
 
 namespace {
@@ -829,8 +841,10 @@ int rt_destroy(rt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->exts, &c->partial,
-                    &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters})
+                    &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters, &c->packed, &c->gathered})
     release(*b);
+  for (rt_comm& m : c->group_comms)
+    if (m.comm) (void)rccl().CommDestroy(m.comm);
   for (auto& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : c->wf_ev)
@@ -1258,6 +1272,168 @@ int rt_tonemap_device(rt_ctx* c, const double* accum_dev, int32_t width, int32_t
   HIP_TRY(c, hipSetDevice(c->device));
   const double inv = 1.0 / (double)(samples == 0 ? 1 : samples);
   HIP_TRY(c, launch_tonemap(accum_dev, width, height, inv, rgb8_dev, s));
+  return RT_OK;
+}
+
+
+// ---- multi-GPU ---------------------------------------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+#define RCCL_TRY(ctx, expr)                                                                       \
+  do {                                                                                            \
+    ncclResult_t r_ = (expr);                                                                     \
+    if (r_ != ncclSuccess) return fail(ctx, RT_E_RCCL, "%s: %s (%s:%d)", #expr, rccl().GetErrorString(r_), \
+                                       __FILE__, __LINE__);                                       \
+  } while (0)
+
+int need_rccl(rt_ctx* c) {
+  if (!rccl().ok()) return fail(c, RT_E_RCCL, "%s", rccl().error.c_str());
+  return RT_OK;
+}
+
+// One rank's part before the gather: its tiles rendered into c->packed (rank 0 also sizes the
+// gathered buffer).  *count = doubles per rank in the gather.
+int shard_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int world, int rank, hipStream_t s,
+                 size_t* count) {
+  int st = check_render_args(c, cam, p);
+  if (st) return st;
+  int32_t n_total = 0, max_tiles = 0;
+  if (rt_tile_layout(cam, world, &n_total, &max_tiles)) return fail(c, RT_E_INVALID, "bad tile layout");
+  *count = (size_t)max_tiles * kTilePixels * 3;
+  if ((st = ensure(c, c->packed, std::max<size_t>(*count, 1) * sizeof(double)))) return st;
+  if (rank == 0 && (st = ensure(c, c->gathered, std::max<size_t>(*count * world, 1) * sizeof(double)))) return st;
+  rt_render_params q = *p;
+  q.tile_rank = rank;
+  q.tile_world = world;
+  const int tiles_y = (cam->image_height + kTile - 1) / kTile;
+  return render_window(c, cam, &q, 0, tiles_y, 0, cam->image_height, 1, static_cast<double*>(c->packed.p), s);
+}
+
+// Root: gathered [world][max_tiles][64][3] -> accum_dev [H][W][3].
+int shard_unpack(rt_ctx* c, const rt_camera* cam, int world, double* accum_dev, hipStream_t s) {
+  int32_t n_total = 0, max_tiles = 0;
+  rt_tile_layout(cam, world, &n_total, &max_tiles);
+  const int tiles_x = (cam->image_width + kTile - 1) / kTile;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, launch_unpack(static_cast<const double*>(c->gathered.p), world, max_tiles, n_total, tiles_x,
+                           cam->image_width, cam->image_height, accum_dev, s));
+  return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]) {
+  if (!id) return RT_E_INVALID;
+  if (!rccl().ok()) return RT_E_RCCL;
+  ncclUniqueId u;
+  static_assert(sizeof u == RT_COMM_ID_BYTES, "ncclUniqueId size");
+  if (rccl().GetUniqueId(&u) != ncclSuccess) return RT_E_RCCL;
+  std::memcpy(id, &u, sizeof u);
+  return RT_OK;
+}
+
+int rt_comm_init_rank(rt_ctx* c, const uint8_t id[RT_COMM_ID_BYTES], int32_t world, int32_t rank, rt_comm** out) {
+  if (!c) return RT_E_INVALID;
+  if (!id || !out || world < 1 || rank < 0 || rank >= world)
+    return fail(c, RT_E_INVALID, "bad communicator arguments (world %d, rank %d)", world, rank);
+  *out = nullptr;
+  int st = need_rccl(c);
+  if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof u);
+  rt_comm* m = new rt_comm();
+  m->world = world;
+  m->rank = rank;
+  m->device = c->device;
+  const ncclResult_t r = rccl().CommInitRank(&m->comm, world, u, rank);
+  if (r != ncclSuccess) {
+    delete m;
+    return fail(c, RT_E_RCCL, "ncclCommInitRank(world %d, rank %d): %s", world, rank, rccl().GetErrorString(r));
+  }
+  *out = m;
+  return RT_OK;
+}
+
+int rt_comm_destroy(rt_comm* m) {
+  if (!m) return RT_OK;
+  if (m->comm && rccl().ok()) {
+    (void)hipSetDevice(m->device);
+    (void)rccl().CommDestroy(m->comm);
+  }
+  delete m;
+  return RT_OK;
+}
+
+int rt_render_sharded(rt_ctx* c, rt_comm* m, const rt_camera* cam, const rt_render_params* p, double* accum_dev,
+                      void* stream) {
+  if (!c) return RT_E_INVALID;
+  if (!m || !m->comm) return fail(c, RT_E_INVALID, "no communicator");
+  if (m->device != c->device) return fail(c, RT_E_INVALID, "communicator of device %d used with device %d", m->device, c->device);
+  if (m->rank == 0 && !accum_dev) return fail(c, RT_E_INVALID, "accum_dev is NULL on the root");
+  hipStream_t s;
+  resolve_stream(c, stream, &s);
+  size_t count = 0;
+  int st = shard_render(c, cam, p, m->world, m->rank, s, &count);
+  if (st) return st;
+  RCCL_TRY(c, rccl().Gather(c->packed.p, m->rank == 0 ? c->gathered.p : nullptr, count, ncclFloat64, 0, m->comm, s));
+  if (m->rank == 0) return shard_unpack(c, cam, m->world, accum_dev, s);
+  return RT_OK;
+}
+
+int rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_camera* cam, const rt_render_params* p,
+                    double* accum_host) {
+  if (!ctxs || n < 1 || !ctxs[0]) return RT_E_INVALID;
+  rt_ctx* root = ctxs[0];
+  if (!cam || !p || !accum_host) return fail(root, RT_E_INVALID, "NULL argument");
+  if (p->tile_world != 1) return fail(root, RT_E_INVALID, "rt_render_multi shards the frame itself (tile_world must be 1)");
+  std::vector<int> devs(n);
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i]) return fail(root, RT_E_INVALID, "ctxs[%d] is NULL", i);
+    devs[i] = ctxs[i]->device;
+    for (int j = 0; j < i; ++j)
+      if (devs[j] == devs[i]) return fail(root, RT_E_INVALID, "device %d appears twice", devs[i]);
+  }
+  int st = need_rccl(root);
+  if (st) return st;
+  if (root->group_devices != devs) {  // (re)build the communicators of this device set
+    for (rt_comm& m : root->group_comms)
+      if (m.comm) (void)rccl().CommDestroy(m.comm);
+    root->group_comms.clear();
+    root->group_devices.clear();
+    std::vector<ncclComm_t> comms(n, nullptr);
+    RCCL_TRY(root, rccl().CommInitAll(comms.data(), n, devs.data()));
+    for (int i = 0; i < n; ++i) root->group_comms.push_back(rt_comm{comms[i], n, i, devs[i]});
+    root->group_devices = devs;
+  }
+  // every device renders its tiles (asynchronous, all devices at once), then one grouped gather
+  std::vector<size_t> count(n);
+  for (int i = 0; i < n; ++i) {
+    if ((st = shard_render(ctxs[i], cam, p, n, i, ctxs[i]->stream, &count[i])))
+      return i ? fail(root, st, "device %d: %s", devs[i], ctxs[i]->err.c_str()) : st;
+  }
+  RCCL_TRY(root, rccl().GroupStart());
+  for (int i = 0; i < n; ++i) {
+    const ncclResult_t r = rccl().Gather(ctxs[i]->packed.p, i == 0 ? root->gathered.p : nullptr, count[i], ncclFloat64, 0,
+                                         root->group_comms[i].comm, ctxs[i]->stream);
+    if (r != ncclSuccess) {
+      (void)rccl().GroupEnd();
+      return fail(root, RT_E_RCCL, "ncclGather (rank %d): %s", i, rccl().GetErrorString(r));
+    }
+  }
+  RCCL_TRY(root, rccl().GroupEnd());
+  const size_t bytes = (size_t)cam->image_width * cam->image_height * 3 * sizeof(double);
+  if ((st = ensure(root, root->accum, bytes))) return st;
+  if ((st = shard_unpack(root, cam, n, static_cast<double*>(root->accum.p), root->stream))) return st;
+  HIP_TRY(root, hipMemcpyAsync(accum_host, root->accum.p, bytes, hipMemcpyDeviceToHost, root->stream));
+  for (int i = n - 1; i >= 0; --i) {
+    HIP_TRY(root, hipSetDevice(ctxs[i]->device));
+    HIP_TRY(root, hipStreamSynchronize(ctxs[i]->stream));
+  }
   return RT_OK;
 }
 

@@ -13,7 +13,8 @@ _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_DIR = os.environ.get("SHIRLEY_LIB_DIR") or os.path.join(_PKG_ROOT, "lib")
 BIN_DIR = os.path.join(_PKG_ROOT, "bin")
 
-RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_OOM, RT_E_UNSUPPORTED = 0, 1, 2, 3, 4
+RT_OK, RT_E_INVALID, RT_E_HIP, RT_E_OOM, RT_E_UNSUPPORTED, RT_E_RCCL = 0, 1, 2, 3, 4, 5
+RT_COMM_ID_BYTES = 128
 RT_GEOM_SPHERE, RT_GEOM_RECT_XY, RT_GEOM_RECT_YZ, RT_GEOM_RECT_XZ, RT_GEOM_RECT_BOX = range(5)
 RT_GEOM_MOVING_SPHERE = 5  # book-2 extension
 RT_MAT_METAL, RT_MAT_DIELECTRIC, RT_MAT_LAMBERTIAN, RT_MAT_DIFFUSE_LIGHT, RT_MAT_FAIRY_LIGHT = range(5)
@@ -132,6 +133,13 @@ RT_SIGNATURES = {
     "rt_scene_hit_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_int32,
                                   C.POINTER(rt_hit)]),
     "rt_synchronize": (C.c_int, [C.c_void_p]),
+    "rt_comm_unique_id": (C.c_int, [C.c_void_p]),
+    "rt_comm_init_rank": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    "rt_comm_destroy": (C.c_int, [C.c_void_p]),
+    "rt_render_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params),
+                                    C.c_void_p, C.c_void_p]),
+    "rt_render_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.POINTER(rt_camera), C.POINTER(rt_render_params),
+                                  C.c_void_p]),
     "rt_counters_get": (C.c_int, [C.c_void_p, C.POINTER(rt_counters)]),
     "rt_bvh_build_host": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int32, C.POINTER(C.c_int32),
                                     C.POINTER(rt_bvh_node), C.POINTER(C.c_int32)]),

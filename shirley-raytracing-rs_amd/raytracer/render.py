@@ -132,10 +132,59 @@ class Device:
     def synchronize(self):
         _check(self._h, N.rt_lib().rt_synchronize(self._h))
 
+    # ---- multi-GPU (rt_comm_*, rt_render_sharded) ----
+    def comm_init_rank(self, unique_id: bytes, world: int, rank: int) -> "Comm":
+        """This device as rank `rank` of a `world`-rank RCCL communicator (one process per GPU)."""
+        if len(unique_id) != N.RT_COMM_ID_BYTES:
+            raise ValueError("unique id must be RT_COMM_ID_BYTES bytes (rt_comm_unique_id)")
+        buf = (C.c_uint8 * N.RT_COMM_ID_BYTES).from_buffer_copy(unique_id)
+        h = C.c_void_p()
+        _check(self._h, N.rt_lib().rt_comm_init_rank(self._h, buf, int(world), int(rank), C.byref(h)))
+        return Comm(h, world, rank)
+
+    def render_sharded(self, comm: "Comm", camera, settings: RenderSettings, accum_ptr: int = 0, stream: int = 0):
+        """This rank's share of the frame + the RCCL gather; rank 0 receives the [H][W][3] sums at accum_ptr."""
+        p = settings.params()
+        _check(self._h, N.rt_lib().rt_render_sharded(self._h, comm.handle, C.byref(camera), C.byref(p),
+                                                     C.c_void_p(accum_ptr or None), C.c_void_p(stream or None)))
+
     def counters(self) -> N.rt_counters:
         c = N.rt_counters()
         _check(self._h, N.rt_lib().rt_counters_get(self._h, C.byref(c)))
         return c
+
+
+class Comm:
+    """An rt_comm (one rank of an RCCL communicator)."""
+
+    def __init__(self, handle, world: int, rank: int):
+        self.handle, self.world, self.rank = handle, world, rank
+
+    def close(self):
+        if getattr(self, "handle", None):
+            N.rt_lib().rt_comm_destroy(self.handle)
+            self.handle = None
+
+    __del__ = close
+
+
+def comm_unique_id() -> bytes:
+    """rt_comm_unique_id: the RCCL id rank 0 creates and hands to every rank."""
+    buf = (C.c_uint8 * N.RT_COMM_ID_BYTES)()
+    code = N.rt_lib().rt_comm_unique_id(buf)
+    if code:
+        raise N.RtError(code, "rt_comm_unique_id failed (RCCL unavailable or no device)")
+    return bytes(buf)
+
+
+def render_multi(devices, camera: N.rt_camera, settings: RenderSettings) -> np.ndarray:
+    """rt_render_multi: the whole frame on several devices of this process (RCCL gather to devices[0])."""
+    out = np.zeros((camera.image_height, camera.image_width, 3), dtype=np.float64)
+    arr = (C.c_void_p * len(devices))(*[d.handle for d in devices])
+    p = settings.params()
+    _check(devices[0].handle, N.rt_lib().rt_render_multi(arr, len(devices), C.byref(camera), C.byref(p),
+                                                         out.ctypes.data))
+    return out
 
 
 def tile_layout(camera: N.rt_camera, world: int):

@@ -1,0 +1,82 @@
+"""Multi-GPU entry points of the C ABI (rt_comm_*, rt_render_sharded, rt_render_multi)
+on the devices a box has.  A one-GPU box forms one-rank communicators: the tile render, the RCCL gather
+(ncclGather to rank 0) and the unpack all run, and the frame must equal rt_render's bit for bit (the
+counter RNG is keyed by the global pixel, so the frame does not depend on the world size).  The
+several-rank data path is covered by test_gpu_parity.py::test_tiles_gather_unpack_equals_full_frame
+(3 and 8 ranks' tiles on one device) and by tests/test_distributed.py (gloo, several processes)."""
+import numpy as np
+import pytest
+
+import raytracer as rt
+from raytracer import _native as N
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED
+
+
+def _frame_setup(gpu):
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    cam = rt.default_camera(53, "std16x9")  # 53 x 29: partial tiles on both axes
+    gpu.upload(scene, "sah")
+    return scene, cam
+
+
+def test_render_multi_one_device_equals_render(gpu):
+    _, cam = _frame_setup(gpu)
+    s = rt.RenderSettings(samples=5, seed=SEED)
+    want = gpu.render(cam, s)
+    got = rt.render_multi([gpu], cam, s)
+    assert np.array_equal(got, want)
+    c = gpu.counters()
+    assert c.samples == cam.image_width * cam.image_height * 5
+    # a second call reuses the cached communicator
+    assert np.array_equal(rt.render_multi([gpu], cam, s), want)
+
+
+def test_render_sharded_one_rank_equals_render_device(gpu):
+    import torch
+    _, cam = _frame_setup(gpu)
+    s = rt.RenderSettings(samples=4, seed=SEED)
+    comm = gpu.comm_init_rank(rt.comm_unique_id(), 1, 0)
+    try:
+        stream = torch.cuda.current_stream().cuda_stream
+        a = torch.full((cam.image_height, cam.image_width, 3), -1.0, dtype=torch.float64, device="cuda")
+        gpu.render_sharded(comm, cam, s, a.data_ptr(), stream)
+        b = torch.zeros_like(a)
+        gpu.render_device(cam, s, b.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert torch.equal(a, b)
+        with pytest.raises(rt.RtError, match="NULL on the root"):
+            gpu.render_sharded(comm, cam, s, 0, stream)
+    finally:
+        comm.close()
+
+
+def test_multi_argument_errors(gpu):
+    _, cam = _frame_setup(gpu)
+    s = rt.RenderSettings(samples=1, seed=SEED)
+    with pytest.raises(rt.RtError, match="appears twice"):
+        rt.render_multi([gpu, gpu], cam, s)
+    with pytest.raises(rt.RtError, match="tile_world"):
+        rt.render_multi([gpu], cam, rt.RenderSettings(samples=1, tile_world=2))
+    with pytest.raises(rt.RtError):
+        gpu.comm_init_rank(rt.comm_unique_id(), 2, 2)  # rank out of range
+    assert N.rt_lib().rt_render_multi(None, 1, None, None, None) == N.RT_E_INVALID
+
+
+def test_cli_gpus_flag(tmp_path):
+    """ray-cli --gpus: one device renders like the default path; more devices than the box has fail
+    with a message (rt_create of the missing device)."""
+    import os
+    import subprocess
+    import torch
+    cli = os.path.join(N.BIN_DIR, "ray-cli")
+    common = ["render", "random", "-w", "64", "-s", "2", "--seed", "0x5EED"]
+    a = str(tmp_path / "a.png")
+    r = subprocess.run([cli] + common + ["-o", a, "--gpus", "1"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    n = torch.cuda.device_count()
+    r = subprocess.run([cli] + common + ["-o", str(tmp_path / "b.png"), "--gpus", str(n + 1)], capture_output=True,
+                       text=True)
+    assert r.returncode == 1 and "rt_create" in r.stderr

@@ -238,3 +238,14 @@ def test_cli_scene_output_and_test_subcommand(tmp_path):
     assert out.returncode == 0 and "nothing to test" in out.stderr
     bad = subprocess.run([cli, "render", "nonsense"], capture_output=True, text=True)
     assert bad.returncode != 0
+
+
+def test_multi_gpu_entry_points_reject_bad_arguments_without_a_device():
+    """rt_render_multi / rt_render_sharded / rt_comm_* validate before touching a device or RCCL."""
+    lib = N.rt_lib()
+    assert lib.rt_render_multi(None, 1, None, None, None) == N.RT_E_INVALID
+    assert lib.rt_render_multi(None, 0, None, None, None) == N.RT_E_INVALID
+    assert lib.rt_render_sharded(None, None, None, None, None, None) == N.RT_E_INVALID
+    assert lib.rt_comm_init_rank(None, None, 1, 0, None) == N.RT_E_INVALID
+    assert lib.rt_comm_destroy(None) == N.RT_OK
+    assert lib.rt_comm_unique_id(None) == N.RT_E_INVALID
