@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--bvh", default="sah", choices=["reference", "sah"])
     ap.add_argument("--sample-chunk", type=int, default=0)
     ap.add_argument("--nodes", default="auto", choices=["auto", "global", "half-lds", "lds"], help="BVH node placement")
-    ap.add_argument("--engine", default="auto", choices=["auto", "megakernel", "wavefront"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "megakernel", "wavefront", "split"])
     ap.add_argument("--timing", action="store_true", help="per-launch HIP-event timing of the wavefront kernels")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of each CPU-baseline leg (full frame at reduced spp; centre rows at full spp)")
@@ -246,7 +246,7 @@ def main():
                                f"{args.seed:#x}", "scene": args.scene, "width": W, "height": H, "spp": args.spp,
                    "max_depth": args.max_depth, "bvh": args.bvh, "parallelism": f"tiles8x8/{world}",
                    "ranks": world, "rehearsal": f"gloo, {world} ranks on {n_dev} GPU(s)" if rehearsal else None,
-                   "engine": {1: "megakernel", 2: "wavefront"}.get(laps[-1][0]), "rounds": laps[-1][1],
+                   "engine": {1: "megakernel", 2: "wavefront", 3: "split"}.get(laps[-1][0]), "rounds": laps[-1][1],
                    "slots": laps[-1][2],
                    "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
                                        "texture": round(laps[-1][5], 3)} if args.timing else None,

@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -68,6 +68,11 @@ enum {
   RT_ENGINE_MEGAKERNEL = 1, /* one persistent kernel runs whole paths, lane-level path regeneration */
   RT_ENGINE_WAVEFRONT = 2,  /* extend / shade / texture kernels over a pool of path slots in HBM;
                              * the host loop blocks until the frame is traced */
+  RT_ENGINE_SPLIT = 3,      /* ABI 5: the megakernel with its traversal decoupled from its shading
+                             * (one block per CU: shading waves post rays to traversal waves through
+                             * LDS queues).  Scenes that fit it: reference primitives only, whole scene
+                             * in LDS; otherwise the call falls back to RT_ENGINE_MEGAKERNEL and
+                             * rt_counters.engine says so */
   RT_ENGINE_TIMING = 0x10   /* flag: time every kernel launch with HIP events (rt_counters *_ms) */
 };
 
@@ -191,7 +196,7 @@ typedef struct rt_counters {
   uint64_t prim_tests;  /* primitive intersection calls */
   double kernel_ms;     /* device time of the trace (all trace kernels of the frame, HIP events) */
   double reduce_ms;     /* device time of the partial-sum reduce kernel */
-  int32_t engine;       /* RT_ENGINE_MEGAKERNEL or RT_ENGINE_WAVEFRONT: the engine that ran */
+  int32_t engine;       /* RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT or RT_ENGINE_SPLIT: the engine that ran */
   int32_t iterations;   /* wavefront: extend/shade/texture rounds (0 for the megakernel) */
   uint64_t slots;       /* wavefront: path slots in flight */
   double extend_ms;     /* wavefront + RT_ENGINE_TIMING: summed device time of wf_extend launches */

@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <string>
 
 #include "../../../include/shirley_host.h"
@@ -76,9 +77,9 @@ int sh_scene_from_json(const char* json, sh_scene** out) {
   if (!json || !out) return fail("NULL argument");
   try {
     Json j = JsonParser(json).parse();
-    sh_scene* s = new sh_scene();
+    std::unique_ptr<sh_scene> s(new sh_scene());  // freed if from_json throws (found by tools/sanitize)
     s->b = SceneBuilder::from_json(j);
-    *out = s;
+    *out = s.release();
   } catch (const std::exception& e) {
     return fail(e.what());
   }
@@ -100,11 +101,11 @@ int sh_scene_builtin(const char* name, uint64_t seed, sh_scene** out) {
 int sh_scene_finalize(const sh_scene* s, uint64_t seed, sh_desc** out) {
   if (!s || !out) return fail("NULL argument");
   try {
-    sh_desc* d = new sh_desc();
+    std::unique_ptr<sh_desc> d(new sh_desc());  // freed if finalize throws
     d->d = s->b.finalize(seed);
     for (size_t i = 0; i < d->d.images.size(); ++i) d->d.images[i].rgb = d->d.image_pixels[i].data();
     d->view = d->d.view();
-    *out = d;
+    *out = d.release();
   } catch (const std::exception& e) {
     return fail(e.what());
   }

@@ -5,6 +5,8 @@
 #pragma once
 
 #include <charconv>
+#include <cstdlib>
+#include <system_error>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -78,25 +80,74 @@ class JsonParser {
     if (s_.compare(i_, n, w) == 0) { i_ += n; return true; }
     return false;
   }
+  // serde_json's recursion limit: deeper nesting is an error, not a stack overflow
+  static constexpr int kMaxDepth = 128;
+  int depth_ = 0;
+  struct Nest {
+    JsonParser& p;
+    explicit Nest(JsonParser& q) : p(q) {
+      if (++p.depth_ > kMaxDepth) p.err("recursion limit exceeded");
+    }
+    ~Nest() { --p.depth_; }
+  };
   Json value() {
     ws();
     if (i_ >= s_.size()) err("unexpected end");
     char c = s_[i_];
-    if (c == '{') return object();
-    if (c == '[') return array();
+    if (c == '{') { Nest n(*this); return object(); }
+    if (c == '[') { Nest n(*this); return array(); }
     if (c == '"') return Json::string(string());
     if (lit("true")) { Json j; j.kind = Json::Bool; j.b = true; return j; }
     if (lit("false")) { Json j; j.kind = Json::Bool; j.b = false; return j; }
     if (lit("null")) return Json();
     return number();
   }
+  // JSON number grammar (RFC 8259 §6, as serde_json accepts it): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+  // validated first, then converted with from_chars (locale-independent, correctly rounded); no
+  // "inf", "nan", hex floats or a leading '+'.  Out-of-range magnitudes are errors, as in serde_json.
   Json number() {
-    const char* b = s_.c_str() + i_;
-    char* e = nullptr;
-    double v = std::strtod(b, &e);
-    if (e == b) err("bad value");
-    i_ += (size_t)(e - b);
+    const size_t b = i_, n = s_.size();
+    auto digit = [&](size_t k) { return k < n && s_[k] >= '0' && s_[k] <= '9'; };
+    size_t k = b;
+    if (k < n && s_[k] == '-') ++k;
+    if (!digit(k)) err("bad value");
+    if (s_[k] == '0') ++k; else while (digit(k)) ++k;
+    if (k < n && s_[k] == '.') {
+      ++k;
+      if (!digit(k)) err("bad number");
+      while (digit(k)) ++k;
+    }
+    if (k < n && (s_[k] == 'e' || s_[k] == 'E')) {
+      ++k;
+      if (k < n && (s_[k] == '+' || s_[k] == '-')) ++k;
+      if (!digit(k)) err("bad number");
+      while (digit(k)) ++k;
+    }
+    double v = 0.0;
+    const auto r = std::from_chars(s_.data() + b, s_.data() + k, v);
+    if (r.ec == std::errc::result_out_of_range) {
+      // underflow to zero / denormal is fine (serde_json rounds), overflow is "number out of range"
+      const std::string t(s_, b, k - b);
+      v = std::strtod(t.c_str(), nullptr);
+      if (std::isinf(v)) err("number out of range");
+    } else if (r.ec != std::errc() || r.ptr != s_.data() + k) {
+      err("bad number");
+    }
+    i_ = k;
     return Json::number(v);
+  }
+  unsigned hex4() {
+    if (i_ + 4 > s_.size()) err("bad \\u escape");
+    unsigned cp = 0;
+    for (int q = 0; q < 4; ++q) {
+      const char h = s_[i_++];
+      cp <<= 4;
+      if (h >= '0' && h <= '9') cp |= (unsigned)(h - '0');
+      else if (h >= 'a' && h <= 'f') cp |= (unsigned)(h - 'a' + 10);
+      else if (h >= 'A' && h <= 'F') cp |= (unsigned)(h - 'A' + 10);
+      else err("bad \\u escape");
+    }
+    return cp;
   }
   std::string string() {
     ++i_;  // "
@@ -115,18 +166,29 @@ class JsonParser {
           case 'n': out += '\n'; break;
           case 'r': out += '\r'; break;
           case 't': out += '\t'; break;
-          case 'u': {
-            if (i_ + 4 > s_.size()) err("bad \\u escape");
-            unsigned cp = (unsigned)std::stoul(s_.substr(i_, 4), nullptr, 16);
-            i_ += 4;
+          case 'u': {  // UTF-16 escape, surrogate pairs combined (lone surrogates are errors)
+            unsigned cp = hex4();
+            if (cp >= 0xDC00 && cp <= 0xDFFF) err("lone surrogate");
+            if (cp >= 0xD800 && cp <= 0xDBFF) {
+              if (!(i_ + 1 < s_.size() && s_[i_] == '\\' && s_[i_ + 1] == 'u')) err("lone surrogate");
+              i_ += 2;
+              const unsigned lo = hex4();
+              if (lo < 0xDC00 || lo > 0xDFFF) err("lone surrogate");
+              cp = 0x10000 + ((cp - 0xD800) << 10) + (lo - 0xDC00);
+            }
             if (cp < 0x80) out += (char)cp;
             else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 0x3F)); }
-            else { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+            else if (cp < 0x10000) { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+            else {
+              out += (char)(0xF0 | (cp >> 18)); out += (char)(0x80 | ((cp >> 12) & 0x3F));
+              out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F));
+            }
             break;
           }
           default: err("bad escape");
         }
       } else {
+        if ((unsigned char)c < 0x20) err("control character in string");
         out += c;
       }
     }

@@ -131,6 +131,15 @@ double surface(const Box& b) {
   return 2.0 * (x * y + y * z + z * x);
 }
 
+// Bin of a centroid, clamped in floating point before the conversion: with extreme coordinates the
+// quotient can be huge, +-inf (ext = inf) or NaN (inf / inf), and converting those to int is undefined
+// (found by tools/sanitize).  NaN goes to bin 0.
+inline int sah_bin(double c, double lo, double ext, int bins) {
+  const double q = (c - lo) / ext * bins;
+  if (!(q > 0.0)) return 0;
+  return q >= bins - 1 ? bins - 1 : (int)q;
+}
+
 struct SahBuilder {
   const std::vector<Box>& boxes;
   std::vector<BuildNode> tree;
@@ -166,8 +175,7 @@ struct SahBuilder {
       int cnt[kBins] = {0};
       bool init[kBins] = {false};
       for (int i = begin; i < end; ++i) {
-        int b = (int)((cen[items[i]][a] - cmn[a]) / ext * kBins);
-        b = std::min(std::max(b, 0), kBins - 1);
+        const int b = sah_bin(cen[items[i]][a], cmn[a], ext, kBins);
         bb[b] = init[b] ? surrounding(bb[b], boxes[items[i]]) : boxes[items[i]];
         init[b] = true;
         cnt[b]++;
@@ -199,8 +207,7 @@ struct SahBuilder {
     } else {
       double ext = cmx[best_axis] - cmn[best_axis];
       auto it = std::partition(items.begin() + begin, items.begin() + end, [&](int idx) {
-        int b = (int)((cen[idx][best_axis] - cmn[best_axis]) / ext * kBins);
-        b = std::min(std::max(b, 0), kBins - 1);
+        const int b = sah_bin(cen[idx][best_axis], cmn[best_axis], ext, kBins);
         return b <= best_split;
       });
       mid = (int)(it - items.begin());

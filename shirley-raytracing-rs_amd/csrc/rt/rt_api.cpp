@@ -23,6 +23,9 @@ namespace rt {
 size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads);
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
+bool split_supported_nt(int nt);
+hipError_t split_prepare(const DScene& S, int nt, int* blocks_per_cu);
+hipError_t launch_split(const KParams& p, int nt, int blocks, hipStream_t stream);
 #ifdef RT_PHASE_TIMING
 void phase_counters_dump();
 #endif
@@ -73,6 +76,8 @@ struct rt_ctx {
   rt_scene_stats stats{};
   int blocks_per_cu = 0;
   int mk_threads = kTraceThreads;  // megakernel block size (kTraceThreadsWide: whole BVH in LDS)
+  int split_nt = 0;                // RT_ENGINE_SPLIT: traversal waves per block (0: scene not eligible)
+  int split_refill = 8;            // idle traversal lanes before a traversal wave claims rays
   // wavefront engine: the scene with its LDS node count sized for the extend block
   DScene wf_scene{};
   int wf_blocks_per_cu = 0;
@@ -90,6 +95,7 @@ struct rt_ctx {
   bool have_timing = false;
   int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0;
   uint64_t last_slots = 0;
+  uint64_t host_samples = 0;  // samples of a frame served without a trace kernel (max_depth == 0)
   double lap_ms[3] = {0, 0, 0};
   // multi-GPU: this rank's packed tiles, the root's gathered buffer, and (root of rt_render_multi)
   // the communicators of the device set last used, kept for the next call
@@ -534,6 +540,7 @@ int default_engine() {
   const char* e = getenv("SHIRLEY_ENGINE");
   if (e && !strcmp(e, "megakernel")) return RT_ENGINE_MEGAKERNEL;
   if (e && !strcmp(e, "wavefront")) return RT_ENGINE_WAVEFRONT;
+  if (e && !strcmp(e, "split")) return RT_ENGINE_SPLIT;
   return RT_ENGINE_MEGAKERNEL;  // measured faster on MI355X
 }
 
@@ -712,8 +719,9 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   int engine = p->engine & 0xf;
   const bool timing = (p->engine & RT_ENGINE_TIMING) != 0;
   if (engine == RT_ENGINE_AUTO) engine = default_engine();
-  if (engine != RT_ENGINE_MEGAKERNEL && engine != RT_ENGINE_WAVEFRONT)
+  if (engine != RT_ENGINE_MEGAKERNEL && engine != RT_ENGINE_WAVEFRONT && engine != RT_ENGINE_SPLIT)
     return fail(c, RT_E_INVALID, "bad engine %d", p->engine);
+  if (engine == RT_ENGINE_SPLIT && c->split_nt == 0) engine = RT_ENGINE_MEGAKERNEL;  // scene not eligible
 
   // samples per unit: ~256 units per resident lane, so that a wave's last units (its lanes finish at
   // different times) cost little.  Short units only add partial-sum traffic (24 B written + read per
@@ -732,7 +740,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     chunk = (int)((samples + n_chunks - 1) / n_chunks);
   }
   chunk = std::max(1, std::min(chunk, samples));
-  if (engine == RT_ENGINE_MEGAKERNEL) {
+  if (engine == RT_ENGINE_MEGAKERNEL || engine == RT_ENGINE_SPLIT) {
     // the megakernel indexes units and partial slots (n_pix * n_chunks) in 32 bits
     const long long max_chunks = n_pix > 0 ? 0xffffffffLL / n_pix : samples;
     if (max_chunks < 1) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
@@ -771,6 +779,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
   HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
   c->last_engine = engine;
+  c->host_samples = 0;
   c->last_chunk = chunk;
   c->last_n_chunks = n_chunks;
   c->last_iters = 0;
@@ -782,7 +791,26 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   } else {
     const int blocks = std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
     HIP_TRY(c, hipEventRecord(c->ev[0], s));
-    if (n_pix > 0) HIP_TRY(c, launch_trace(kp, blocks, c->mk_threads, s));
+    if (n_pix > 0 && p->max_depth == 0) {
+      // ray_color's loop never runs (render.rs:30): every sample is black.  The megakernel's exit
+      // test assumes a held unit always has an active path (true for max_depth > 0), so this case
+      // is served here: all-zero partials, reduced like any frame; the samples counter counts the
+      // window's in-image pixels of this rank's tiles, as the kernel would.
+      HIP_TRY(c, hipMemsetAsync(kp.partial, 0, (size_t)n_pix * n_chunks * 3 * sizeof(double), s));
+      uint64_t inside = 0;
+      for (long long lt = 0; lt < L.n_tiles_rank; ++lt) {
+        const long long gt = lt * p->tile_world + p->tile_rank;
+        const int tx = (int)(gt % L.tiles_x), ty = ty0 + (int)(gt / L.tiles_x);
+        const int w = std::min(kTile, cam->image_width - tx * kTile), h = std::min(kTile, cam->image_height - ty * kTile);
+        if (w > 0 && h > 0) inside += (uint64_t)w * (uint64_t)h;
+      }
+      c->host_samples = inside * (uint64_t)samples;
+    } else if (n_pix > 0 && engine == RT_ENGINE_SPLIT) {
+      kp.split_refill = c->split_refill;
+      HIP_TRY(c, launch_split(kp, c->split_nt, c->cu_count, s));
+    } else if (n_pix > 0) {
+      HIP_TRY(c, launch_trace(kp, blocks, c->mk_threads, s));
+    }
     HIP_TRY(c, hipEventRecord(c->ev[1], s));
   }
   if (n_pix > 0)
@@ -1053,6 +1081,16 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->has_perlin = false;
   for (int i = 0; i < d->n_textures; ++i) c->has_perlin |= d->textures[i].kind == RT_TEX_PERLIN;
   c->wf_blocks_per_cu = wbpc;
+  // RT_ENGINE_SPLIT: the wide block's scene plus traversal stacks and ray slots in LDS
+  c->split_nt = 0;
+  if (c->mk_threads == kTraceThreadsWide && S.n_lds_prims == d->n_objects && !S.exts) {
+    int nt = 8;
+    if (const char* e = getenv("SHIRLEY_SPLIT_NT")) nt = atoi(e);  // tuning
+    if (const char* e = getenv("SHIRLEY_SPLIT_REFILL")) c->split_refill = std::max(1, atoi(e));  // tuning
+    int sb = 0;
+    if (split_supported_nt(nt)) HIP_TRY(c, split_prepare(S, nt, &sb));
+    if (sb >= 1) c->split_nt = nt;
+  }
 
   c->stats.n_objects = d->n_objects;
   c->stats.n_nodes = (int32_t)tree.nodes.size();
@@ -1188,6 +1226,7 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
   HIP_TRY(c, hipEventSynchronize(c->ev[2]));
   std::vector<DCounters> dc(kCounterSlots);
   HIP_TRY(c, hipMemcpy(dc.data(), c->counters.p, kCounterSlots * sizeof(DCounters), hipMemcpyDeviceToHost));
+  out->samples = c->host_samples;
   for (const DCounters& k : dc) {
     out->samples += k.samples;
     out->segments += k.segments;

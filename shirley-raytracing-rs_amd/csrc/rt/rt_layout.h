@@ -179,6 +179,7 @@ struct KParams {
   double* partial;               // [n_chunks][n_tiles_rank*64][3]
   unsigned long long* unit_counter;  // work-queue head (one 64-unit batch per fetch)
   DCounters* counters;
+  int32_t split_refill;          // split_kernel: idle traversal lanes before a wave claims rays (>= 1)
 };
 
 // ---- wavefront engine (wavefront.hip): path state of P slots as structure-of-arrays in HBM ----

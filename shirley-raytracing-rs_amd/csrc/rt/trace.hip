@@ -158,10 +158,11 @@ __global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void
       if (!active) sum = sum + em;  // max_depth == 0: ray_color returns black (render.rs:30)
     }
     if (!__any(active)) {
-      // done only when the pool is drained AND no lane still holds a unit: with max_depth == 0 a
-      // lane's samples never become active, so its unit advances (and publishes) in these
-      // iterations alone
-      if (exhausted && __ballot(has_unit) == 0ull) break;
+      // with max_depth > 0 a lane holding a unit is active here (a unit whose last sample ended
+      // was published in step 1, a new or continuing one started a sample in step 3), so no lane
+      // holds a unit once none is active and the pool is drained.  max_depth == 0 (no path ever
+      // becomes active) never reaches this kernel: render_window writes its black frame itself.
+      if (exhausted) break;
       continue;
     }
     // 4. one ray_color iteration (render.rs:30-46): closest hit, then emitted + scatter or sky

@@ -23,7 +23,7 @@ RT_TEX_SOLID, RT_TEX_CHECKER, RT_TEX_PERLIN, RT_TEX_IMAGE = range(4)
 RT_SKY_ABOVE, RT_SKY_FLAT, RT_SKY_NONE = range(3)
 RT_BVH_REFERENCE, RT_BVH_SAH = 0, 1
 RT_BVH_NODES_GLOBAL, RT_BVH_NODES_HALF_LDS, RT_BVH_NODES_LDS = 0x100, 0x200, 0x400
-RT_ENGINE_AUTO, RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_TIMING = 0, 1, 2, 0x10
+RT_ENGINE_AUTO, RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_SPLIT, RT_ENGINE_TIMING = 0, 1, 2, 3, 0x10
 RT_TRAVERSAL_BINARY, RT_TRAVERSAL_RENDER = 0, 1
 
 _d3 = C.c_double * 3

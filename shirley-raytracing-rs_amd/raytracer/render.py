@@ -29,10 +29,11 @@ class RenderSettings:
     sample_chunk: int = 0
     tile_rank: int = 0
     tile_world: int = 1
-    engine: str = "auto"   # auto | megakernel | wavefront
+    engine: str = "auto"   # auto | megakernel | wavefront | split
     timing: bool = False   # per-launch HIP-event timing of the wavefront kernels (rt_counters *_ms)
 
-    ENGINES = {"auto": N.RT_ENGINE_AUTO, "megakernel": N.RT_ENGINE_MEGAKERNEL, "wavefront": N.RT_ENGINE_WAVEFRONT}
+    ENGINES = {"auto": N.RT_ENGINE_AUTO, "megakernel": N.RT_ENGINE_MEGAKERNEL, "wavefront": N.RT_ENGINE_WAVEFRONT,
+               "split": N.RT_ENGINE_SPLIT}
 
     def params(self) -> N.rt_render_params:
         p = N.rt_render_params()

@@ -13,8 +13,8 @@ at exactly the same t, which changes one whole path.  The test therefore demands
     0.9994, 1200-wide rows 0.9915, every other scene 1.0),
   * every channel within TOL = 1e-10 * spp absolute of the oracle, except at most 0.1 % of pixels
     (a flipped path changes one sample by up to the path's radiance).
-Both trace engines (RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT) run the same binary64 code on the same
-counter-RNG streams, so their frames must be bit-identical to each other.
+The trace engines (RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_SPLIT) run the same binary64
+code on the same counter-RNG streams, so their frames must be bit-identical to each other.
 """
 import ctypes as C
 
@@ -27,7 +27,17 @@ import raytracer as rt
 pytestmark = pytest.mark.gpu
 
 SEED = 0x5EED
-ENGINES = ["megakernel", "wavefront"]
+ENGINES = ["megakernel", "wavefront", "split"]
+ENGINE_ID = {"megakernel": 1, "wavefront": 2, "split": 3}
+# RT_ENGINE_SPLIT serves reference scenes whose whole scene fits in LDS; book-2 scenes fall back to
+# the megakernel (rt_counters.engine reports the engine that ran)
+SPLIT_FALLBACK = {"final:6:60", "final"}
+
+
+def engine_ran(cnt, engine, name=""):
+    if engine == "split" and name in SPLIT_FALLBACK:
+        return cnt.engine == ENGINE_ID["megakernel"]
+    return cnt.engine == ENGINE_ID[engine]
 
 
 def _log_fraction(exact, bad, shape):
@@ -78,12 +88,13 @@ def test_render_matches_oracle(gpu, name, width, aspect):
                                                 engine=engine))
         check_parity(img, ora, spp, frac_exact=EXACT_MIN[name])
         cnt = gpu.counters()
-        assert cnt.engine == {"megakernel": 1, "wavefront": 2}[engine]
+        assert engine_ran(cnt, engine, name)
         assert cnt.samples == cam.image_width * cam.image_height * spp == ocnt.samples
         # segment counts follow from the (identical) paths
         assert abs(int(cnt.segments) - int(ocnt.segments)) <= 0.001 * ocnt.segments
         imgs[engine] = img
-    assert np.array_equal(imgs["megakernel"], imgs["wavefront"])
+    for engine in ENGINES[1:]:
+        assert np.array_equal(imgs["megakernel"], imgs[engine]), engine
 
 
 @pytest.mark.parametrize("name,aspect", [("random", "std16x9"), ("cornell", "square"), ("earth", "square"),
@@ -349,7 +360,7 @@ def test_edge_cases(gpu, engine):
         gpu.render(cam, rt.RenderSettings(engine=engine, samples=-1))
     with pytest.raises(rt.RtError):
         gpu.render_scanlines(cam, rt.RenderSettings(engine=engine, samples=1), 5, 100)
-    if engine == "megakernel":  # 64 pixels x (2^26 + 1) one-sample units >= 2^32: refused before any work
+    if engine in ("megakernel", "split"):  # 64 pixels x (2^26 + 1) one-sample units >= 2^32: refused before any work
         with pytest.raises(rt.RtError, match="2\\^32"):
             gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1))
 
