@@ -146,7 +146,44 @@ struct SahBuilder {
   std::vector<int> items;
   std::vector<std::array<double, 3>> cen;
 
+  bool sweep = false;  // exact SAH over every object boundary instead of 32 centroid bins
+  std::vector<int> tmp;
+  std::vector<double> right_sa;
+
   explicit SahBuilder(const std::vector<Box>& b) : boxes(b) {}
+
+  // Exact sweep: per axis, the objects sorted by centroid (ties by index), every split point
+  // evaluated with prefix / suffix bounding boxes; items[begin, end) left in the best axis's order.
+  // Returns the split position, or -1 when no split separates anything (all centroids equal).
+  int sweep_split(int begin, int end) {
+    const int n = end - begin;
+    double best_cost = INFINITY;
+    int best_axis = -1, best_i = -1;
+    right_sa.resize(n);
+    for (int a = 0; a < 3; ++a) {
+      tmp.assign(items.begin() + begin, items.begin() + end);
+      std::sort(tmp.begin(), tmp.end(), [&](int x, int y) {
+        return cen[x][a] < cen[y][a] || (cen[x][a] == cen[y][a] && x < y);
+      });
+      Box acc = boxes[tmp[n - 1]];
+      for (int i = n - 1; i >= 1; --i) {  // right_sa[i]: objects [i, n)
+        if (i < n - 1) acc = surrounding(acc, boxes[tmp[i]]);
+        right_sa[i] = surface(acc);
+      }
+      acc = boxes[tmp[0]];
+      for (int i = 1; i < n; ++i) {  // split before object i: left [0, i), right [i, n)
+        if (i > 1) acc = surrounding(acc, boxes[tmp[i - 1]]);
+        if (cen[tmp[i - 1]][a] == cen[tmp[i]][a]) continue;  // not a separating plane
+        const double cost = surface(acc) * i + right_sa[i] * (n - i);
+        if (cost < best_cost) { best_cost = cost; best_axis = a; best_i = i; }
+      }
+    }
+    if (best_axis < 0) return -1;
+    std::sort(items.begin() + begin, items.begin() + end, [&](int x, int y) {
+      return cen[x][best_axis] < cen[y][best_axis] || (cen[x][best_axis] == cen[y][best_axis] && x < y);
+    });
+    return begin + best_i;
+  }
 
   int32_t build(int begin, int end) {
     int n = end - begin;
@@ -157,6 +194,19 @@ struct SahBuilder {
       leaf.lhs = leaf.rhs = -1;
       tree.push_back(leaf);
       return (int32_t)tree.size() - 1;
+    }
+    if (sweep) {
+      int mid = sweep_split(begin, end);
+      if (mid < 0) mid = begin + n / 2;
+      const int32_t self = (int32_t)tree.size();
+      tree.push_back(BuildNode{});
+      const int32_t l = build(begin, mid);
+      const int32_t r = build(mid, end);
+      tree[self].leaf = -1;
+      tree[self].lhs = l;
+      tree[self].rhs = r;
+      tree[self].box = surrounding(tree[l].box, tree[r].box);
+      return self;
     }
     double cmn[3], cmx[3];
     for (int k = 0; k < 3; ++k) { cmn[k] = INFINITY; cmx[k] = -INFINITY; }
@@ -249,9 +299,10 @@ BuiltTree build_reference_tree(const std::vector<Box>& boxes) {
   return out;
 }
 
-BuiltTree build_sah_tree(const std::vector<Box>& boxes) {
+BuiltTree build_sah_tree(const std::vector<Box>& boxes, bool sweep) {
   BuiltTree out;
   SahBuilder b(boxes);
+  b.sweep = sweep;
   for (int i = 0; i < (int)boxes.size(); ++i) {
     const Box& x = boxes[i];
     bool never = false;
