@@ -50,6 +50,8 @@ def parse():
                     help="target wall time of each CPU-baseline leg (full frame at reduced spp; centre rows at full spp)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use (cgroup-aware)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the one-frame measurements of BASELINE.json's other configs (N=1 only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (gloo only to rehearse several ranks on one GPU)")
     return ap.parse_args()
@@ -113,6 +115,56 @@ def cpu_baseline(scene, cam, args):
                                 "sample": f"rows [{r0}, {r0 + rows}) x {W} @ {args.spp} spp (full spp), "
                                           f"{cnt2.samples} samples, {dt2:.1f} s wall"},
             "host": info}
+
+
+# BASELINE.json configs other than the headline (configs[1]), each one full frame at its stated size
+# and spp on this GPU: (key, scene, width, aspect, spp, note).  Config 5's book-2 final_scene is the
+# book-2 extension scene (the reference has none); its ~10k-primitive stand-in from the
+# reference's own benches (gen_spheres, benches/my_benchmark.rs:35-60) is measured beside it.
+OTHER_CONFIGS = [
+    ("cfg1", "random", 400, "std16x9", 50, "book-1 random_scene 400x225 @ 50 spp"),
+    ("cfg3", "earth", 800, "square", 1000, "earth-texture sphere 800x800 @ 1000 spp"),
+    ("cfg4", "cornell", 600, "square", 10000, "Cornell box 600x600 @ 10000 spp"),
+    ("cfg5_final", "final", 1920, "std16x9", 2000, "book-2 final_scene 1920x1080 @ 2000 spp, 1 GPU of the 8"),
+    ("cfg5_spheres", "spheres", 1920, "std16x9", 2000, "gen_spheres 22^3 = 10648 spheres 1920x1080 @ 2000 spp, 1 GPU"),
+]
+
+
+def configs_block(args, dev, torch, rt):
+    """One timed full frame of every other BASELINE config on this GPU, after one untimed frame of the
+    same size and spp (it sizes the per-render scratch, so no allocation falls in the timed frame),
+    plus config 1's CPU leg as BASELINE.md specifies it (the oracle, single thread, full frame)."""
+    out = {}
+    stream = torch.cuda.current_stream()
+    for key, name, width, aspect, spp, note in OTHER_CONFIGS:
+        scene = rt.SceneBuilder.builtin(name, args.seed).finalize(args.seed)
+        cam = rt.scene_camera(name, width, aspect)
+        W, H = cam.image_width, cam.image_height
+        dev.upload(scene, args.bvh)
+        accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+        dev.render_device(cam, rt.RenderSettings(samples=spp, max_reflect=args.max_depth, seed=args.seed),
+                          accum.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        dev.render_device(cam, rt.RenderSettings(samples=spp, max_reflect=args.max_depth, seed=args.seed),
+                          accum.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        c = dev.counters()
+        out[key] = {"workload": note, "value": round(W * H * spp / dt / 1e6, 3), "unit": "Msamples/s",
+                    "ms_per_frame": round(dt * 1e3, 3), "kernel_ms": round(c.kernel_ms, 3),
+                    "segments_per_sample": round(c.segments / max(c.samples, 1), 4),
+                    "engine": {1: "megakernel", 2: "wavefront", 3: "split"}.get(c.engine)}
+        if key == "cfg1" and not args.no_cpu:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_lib as O
+            t0 = time.perf_counter()
+            _, cnt = O.OracleScene(scene).render(cam, O.params(spp, args.max_depth, args.seed), threads=1)
+            dt = time.perf_counter() - t0
+            out[key]["cpu_single_thread"] = {"value": round(cnt.samples / dt / 1e6, 4), "unit": "Msamples/s",
+                                             "sample": f"full frame {W}x{H} @ {spp} spp, 1 thread, {dt:.1f} s "
+                                                       "(f64 C oracle, a proxy for the Rust reference)"}
+    return out
 
 
 def valu_block(segments, k_ms, W, H, args):
@@ -265,6 +317,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(scene, cam, args)
+    if world == 1 and not args.no_configs:  # (after the timed region; the headline scene is replaced)
+        line["configs"] = configs_block(args, dev, torch, rt)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:
