@@ -24,7 +24,25 @@ __device__ __forceinline__ v3 hmul(v3 a, v3 b) { return V(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ v3 scale(v3 a, double s) { return V(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ double dot(v3 a, v3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ double len2(v3 a) { return dot(a, a); }
-__device__ __forceinline__ double len(v3 a) { return sqrt(len2(a)); }
+// Correctly rounded binary64 sqrt with a shorter common path.  hipcc lowers sqrt(x) on gfx950 to:
+// x' = x < 2^-767 ? x * 2^256 : x, r = rsq(x'), g = x' r, h = r / 2, e = fma(-h, g, 0.5),
+// g = fma(g, e, g), d = fma(-g, g, x'), h = fma(h, e, h), g = fma(d, h, g), d = fma(-g, g, x'),
+// g = fma(d, h, g), result = scale g back by 2^-128, and x' itself when x' is +-0 or +inf.  For x in
+// [2^-767, DBL_MAX] neither the scaling nor the pass-through applies, so the same rsq + Newton
+// sequence alone gives the same bits (checked on the GPU by tools/divcheck.hip); other x take sqrt().
+__device__ __forceinline__ double sqrt_rn(double x) {
+  if (!(x >= 0x1p-767 && x <= 1.7976931348623157e308)) return sqrt(x);
+  const double r = __builtin_amdgcn_rsq(x);
+  double g = x * r, h = r * 0.5;
+  const double e = __builtin_fma(-h, g, 0.5);
+  g = __builtin_fma(g, e, g);
+  double d = __builtin_fma(-g, g, x);
+  h = __builtin_fma(h, e, h);
+  g = __builtin_fma(d, h, g);
+  d = __builtin_fma(-g, g, x);
+  return __builtin_fma(d, h, g);
+}
+__device__ __forceinline__ double len(v3 a) { return sqrt_rn(len2(a)); }
 __device__ __forceinline__ v3 unit(v3 a) {
   double n = len(a);
   return V(a.x / n, a.y / n, a.z / n);
@@ -242,10 +260,33 @@ __device__ __forceinline__ bool sphere_t(const double* p, v3 o, v3 d, double a, 
   double c = len2(oc) - p[3] * p[3];
   double disc = half_b * half_b - a * c;
   if (disc < 0.0) return false;
-  double sqrt_d = sqrt(disc);
+  double sqrt_d = sqrt_rn(disc);
   double root = (-half_b - sqrt_d) / a;
   if (root < t_min || t_max < root) {
     root = (-half_b + sqrt_d) / a;
+    if (root < t_min || t_max < root) return false;
+  }
+  t = root;
+  return true;
+}
+// The same with both root divisions by a through a per-ray shared reciprocal (exact: div_recip's
+// range, checked per numerator; a itself is in range when ra_ok).
+__device__ __forceinline__ double div_by(double n, const Recip& R, bool ok) {
+  const double m = fabs(n);
+  if (ok && m >= 0x1p-300 && m <= 0x1p300) return div_recip(n, R);
+  return n / R.b;
+}
+__device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Recip& ra, bool ra_ok, double t_min,
+                                           double t_max, double& t) {
+  v3 oc = o - V(p[0], p[1], p[2]);
+  double half_b = dot(oc, d);
+  double c = len2(oc) - p[3] * p[3];
+  double disc = half_b * half_b - ra.b * c;
+  if (disc < 0.0) return false;
+  double sqrt_d = sqrt_rn(disc);
+  double root = div_by(-half_b - sqrt_d, ra, ra_ok);
+  if (root < t_min || t_max < root) {
+    root = div_by(-half_b + sqrt_d, ra, ra_ok);
     if (root < t_min || t_max < root) return false;
   }
   t = root;
@@ -853,7 +894,7 @@ __device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned
 
 template <int MODE, bool EXT>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
-                                            RaySigns ns, double a, double t_min, unsigned lm, int c0, int c1,
+                                            RaySigns ns, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, double& t_best, float& tmaxf, int& best,
                                             int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
   // lm: spread mask of hit leaf children (bit 8 i + 7: child i).  A leaf's child word is
@@ -873,7 +914,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double t;
     PH_COUNT(3);
     ++ptests;
-    if (sphere_t(pr.p, o, d, a, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
+    if (sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
 #pragma unroll 1
   while (rect) {
@@ -989,7 +1030,7 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
 }
 template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
-                                      v3 inv, RaySigns ns, const RayF& rf, double a, double t_min, int node,
+                                      v3 inv, RaySigns ns, const RayF& rf, const Recip& ra, bool ra_ok, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
                                       unsigned& top, unsigned* stk, const Rng& rk, uint64_t seed,
                                       unsigned& visits, unsigned& ptests) {
@@ -999,7 +1040,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
                                         visits);
   if (lm) PH_COUNT(1);
   if (lm)
-    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, a, t_min, lm, ch.x, ch.y, ch.z, ch.w, t_best, tmaxf, best,
+    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, t_best, tmaxf, best,
                            face_best, rk, seed, ptests);
   return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
 }
@@ -1019,6 +1060,8 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
   const RaySigns ns = ray_signs(inv);
   const RayF rf = ray_f(S, o, inv);
   const double a = len2(d);
+  const Recip ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_r)
+  const bool ra_ok = a >= 0x1p-300 && a <= 0x1p300;
   float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;
@@ -1030,7 +1073,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
 #ifdef RT_PHASE_TIMING
     ++g_trav_lane_steps;
 #endif
-    node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, a, t_min, node, t_best, tmaxf, best,
+    node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, ra, ra_ok, t_min, node, t_best, tmaxf, best,
                                 face_best, sp, top, stk, rk, seed, visits, ptests);
   }
   return best;
@@ -1039,7 +1082,9 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
 // Step-wise form for wf_extend4, where a ray's traversal state lives across loop iterations.
 struct Trav4 {
   v3 inv;
-  double a, t_best;
+  Recip ra;  // ra.b = |d|^2 (sphere_t_r)
+  bool ra_ok;
+  double t_best;
   float tmaxf;
   int best, face, node, sp, steps;
   unsigned top;  // the stack's top entry (node4_next)
@@ -1051,7 +1096,8 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
   T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   T.ns = ray_signs(T.inv);
   T.rf = ray_f(S, o, T.inv);
-  T.a = len2(d);
+  T.ra = recip(len2(d));
+  T.ra_ok = T.ra.b >= 0x1p-300 && T.ra.b <= 0x1p300;
   T.t_best = t_max;
   T.tmaxf = tmax_f32(t_max);
   T.best = -1;
@@ -1068,7 +1114,7 @@ __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_n
                                            v3 d, double t_min, Trav4& T, unsigned* stk, const Rng& rk,
                                            uint64_t seed, unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
-  T.node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.a, t_min, T.node, T.t_best,
+  T.node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.ra, T.ra_ok, t_min, T.node, T.t_best,
                                 T.tmaxf, T.best, T.face, T.sp, T.top, stk, rk, seed, visits, ptests);
   return T.node < 0;
 }

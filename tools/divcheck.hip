@@ -1,5 +1,5 @@
 // Bit-identity check of the shared-reciprocal division (rt_device.h: recip / div_recip / unit_fast)
-// against the compiler's binary64 division, on the GPU.  Usage: divcheck [log2 pairs per launch] [launches]
+// against the compiler's binary64 division, and of sqrt_rn against the compiler's sqrt, on the GPU.  Usage: divcheck [log2 pairs per launch] [launches]
 // Pairs: random signs, random 52-bit mantissas (a share with all-ones / all-zeros / near-one patterns),
 // exponents uniform in [-300, 300]; vectors likewise with independent component exponents in a
 // +-40 window.  Prints the mismatch counts; exit code 1 if any.
@@ -38,24 +38,41 @@ __global__ void check(uint64_t base, unsigned long long* bad) {
   const int ec = (int)((h3 >> 32) % 521) - 260;
   const uint64_t g1 = mix(i * 5 + 11), g2 = mix(i * 5 + 12), g3 = mix(i * 5 + 13);
   const v3 v = V(make(g1, ec + (int)(g1 % 81) - 40), make(g2, ec + (int)(g2 % 81) - 40), make(g3, ec + (int)(g3 % 81) - 40));
-  const v3 u0 = unit(v), u1 = unit_fast(v);
+  const v3 u0 = V(v.x / sqrt(len2(v)), v.y / sqrt(len2(v)), v.z / sqrt(len2(v))), u1 = unit_fast(v);
   if (__double_as_longlong(u0.x) != __double_as_longlong(u1.x) || __double_as_longlong(u0.y) != __double_as_longlong(u1.y) ||
       __double_as_longlong(u0.z) != __double_as_longlong(u1.z))
     atomicAdd(&bad[1], 1ull);
+  // sqrt_rn against the compiler's sqrt: positive x over the whole exponent range (denormals, the
+  // 2^-767 scaling edge, huge values) plus the special values now and then
+  const uint64_t hs = mix(i * 3 + 17);
+  const int es = (int)(hs % 2100) - 1075;  // exponents -1075 .. 1024: denormals .. inf / NaN patterns
+  double x = es < -1022 ? __longlong_as_double((long long)(hs >> 12)) : make(hs & ~(1ull << 63), es < 1024 ? es : 1023);
+  switch ((hs >> 56) & 63) {
+    case 0: x = 0.0; break;
+    case 1: x = -0.0; break;
+    case 2: x = __builtin_inf(); break;
+    case 3: x = -1.0; break;
+    case 4: x = __builtin_nan(""); break;
+    case 5: x = 0x1p-767; break;
+    case 6: x = __longlong_as_double(0x1000000000000000ll - 1); break;  // just below 2^-767
+    default: break;
+  }
+  const double s0 = sqrt(x), s1 = sqrt_rn(x);
+  if (__double_as_longlong(s0) != __double_as_longlong(s1) && !(s0 != s0 && s1 != s1)) atomicAdd(&bad[2], 1ull);
 }
 
 int main(int argc, char** argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 26;
   const int launches = argc > 2 ? atoi(argv[2]) : 16;
   unsigned long long* bad;
-  if (hipMalloc(&bad, 16) != hipSuccess) return 2;
-  (void)hipMemset(bad, 0, 16);
+  if (hipMalloc(&bad, 24) != hipSuccess) return 2;
+  (void)hipMemset(bad, 0, 24);
   const uint64_t per = 1ull << lg;
   for (int l = 0; l < launches; ++l)
     hipLaunchKernelGGL(check, dim3((unsigned)(per / 256)), dim3(256), 0, 0, (uint64_t)l * per, bad);
-  unsigned long long h[2];
-  if (hipMemcpy(h, bad, 16, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-  printf("divcheck: %llu pairs, %llu division mismatches, %llu unit mismatches\n",
-         (unsigned long long)(per * launches), h[0], h[1]);
-  return (h[0] || h[1]) ? 1 : 0;
+  unsigned long long h[3];
+  if (hipMemcpy(h, bad, 24, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+  printf("divcheck: %llu pairs, %llu division mismatches, %llu unit mismatches, %llu sqrt mismatches\n",
+         (unsigned long long)(per * launches), h[0], h[1], h[2]);
+  return (h[0] || h[1] || h[2]) ? 1 : 0;
 }
