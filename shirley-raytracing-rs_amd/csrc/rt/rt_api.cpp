@@ -1106,6 +1106,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS) &&
                     !getenv("SHIRLEY_NO_WIDE");  // tuning
   c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
+  // book-2 scenes: the EXT instance spills ~80 VGPRs at 4 waves per SIMD (1024 threads) and none at 3
+  // (768 threads, 165 VGPRs): final_scene +3.3 % (profiles/r02/wide3.txt).  SHIRLEY_WIDE4: tuning switch.
+  if (wide && !exts.empty() && !getenv("SHIRLEY_WIDE4")) c->mk_threads = kTraceThreadsWide3;
   S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
   S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4F), nodes4.size());
   // primitives too, when they fit beside the wide block's tree and stacks (leaf tests from LDS)
@@ -1135,7 +1138,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   if (wbpc < 1) return fail(c, RT_E_UNSUPPORTED, "wavefront extend kernel does not fit on a CU");
   c->wf_scene = W;
   c->wf_wide = false;
-  if (c->mk_threads == kTraceThreadsWide && S.n_lds_prims > 0 && !getenv("SHIRLEY_WF_EXTEND2")) {
+  if (c->mk_threads >= kTraceThreadsWide3 && S.n_lds_prims > 0 && !getenv("SHIRLEY_WF_EXTEND2")) {
     int b4 = 0;
     HIP_TRY(c, wf_prepare4(S, &b4));
     if (b4 >= 1) {
@@ -1166,7 +1169,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->stats.n_leaves = leaves;
   c->stats.depth = depth;
   c->stats.n_nodes4 = S.n_nodes4;
-  c->stats.wide_block = c->mk_threads == kTraceThreadsWide ? 1 : 0;
+  c->stats.wide_block = c->mk_threads >= kTraceThreadsWide3 ? 1 : 0;
   c->stats.origin_limit = S.origin_limit;
   c->stats.device_bytes = (int64_t)(nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim) +
                                     mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex) +
@@ -1267,7 +1270,7 @@ int rt_scene_hit_ex(rt_ctx* c, const double* rays, int32_t n, double t_min, doub
   if (!st) {
     const double* rd = static_cast<const double*>(r.p);
     hipError_t e = traversal == RT_TRAVERSAL_RENDER
-                       ? launch_hit4(c->scene, c->mk_threads == kTraceThreadsWide, rd, n, t_min, t_max, h.p, c->stream)
+                       ? launch_hit4(c->scene, c->mk_threads >= kTraceThreadsWide3, rd, n, t_min, t_max, h.p, c->stream)
                        : launch_hit(c->scene, rd, n, t_min, t_max, h.p, c->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(out, h.p, (size_t)n * sizeof(rt_hit), hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);

@@ -14,6 +14,7 @@ constexpr int kTile = 8;
 constexpr int kTilePixels = kTile * kTile;  // == wavefront size
 constexpr int kTraceThreads = 256;      // megakernel block, BVH in L1/L2: 4 waves, several blocks per CU
 constexpr int kTraceThreadsWide = 1024; // megakernel block holding the whole BVH in LDS: 16 waves (4 per SIMD), one per CU
+constexpr int kTraceThreadsWide3 = 768; // the same at 3 waves per SIMD (168 VGPRs): book-2 (EXT) scenes
 constexpr int kHitThreads = 256;    // rt_scene_hit kernel
 constexpr int kWave = 64;
 constexpr int kLdsBytes = 160 * 1024;  // LDS per CU (gfx950)

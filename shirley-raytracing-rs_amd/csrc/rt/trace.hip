@@ -39,8 +39,16 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 // 4 waves per SIMD, 128 VGPRs).  HIP's second launch-bounds argument is the minimum waves per SIMD.
 // EXT: the scene has book-2 primitives; their code is compiled into separate
 // instances so that reference scenes keep the kernel's register allocation.
+// (tuning switches for A/B builds: minimum waves per SIMD of the 256-thread instances)
+#ifndef RT_NARROW_WAVES_EXT
+#define RT_NARROW_WAVES_EXT 4
+#endif
+#ifndef RT_NARROW_WAVES
+#define RT_NARROW_WAVES 4
+#endif
 template <int THREADS, int MODE, bool EXT>
-__global__ __launch_bounds__(THREADS, THREADS == kTraceThreadsWide ? 1 : 4) void trace_kernel(KParams P) {
+__global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : (EXT ? RT_NARROW_WAVES_EXT : RT_NARROW_WAVES))
+void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
   DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
@@ -501,6 +509,11 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
     if (S.n_lds_prims > 0) return occupancy_impl<kTraceThreadsWide, kSceneLds>(S, blocks_per_cu);
     return occupancy_impl<kTraceThreadsWide, kNodesLds>(S, blocks_per_cu);
   }
+  if (threads == kTraceThreadsWide3) {  // book-2 scenes only (rt_api.cpp)
+    if (node_mode4(S) != kNodesLds || !S.exts) return hipErrorInvalidValue;
+    if (S.n_lds_prims > 0) return occupancy_impl1<kTraceThreadsWide3, kSceneLds, true>(S, blocks_per_cu);
+    return occupancy_impl1<kTraceThreadsWide3, kNodesLds, true>(S, blocks_per_cu);
+  }
   switch (node_mode4(S)) {
     case kNodesLds: return occupancy_impl<kTraceThreads, kNodesLds>(S, blocks_per_cu);
     case kNodesGlobal: return occupancy_impl<kTraceThreads, kNodesGlobal>(S, blocks_per_cu);
@@ -515,6 +528,14 @@ hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t s
       launch_trace1<kTraceThreadsWide, kSceneLds>(p, blocks, lds, stream);
     else
       launch_trace1<kTraceThreadsWide, kNodesLds>(p, blocks, lds, stream);
+    return hipGetLastError();
+  }
+  if (threads == kTraceThreadsWide3) {
+    if (!p.scene.exts) return hipErrorInvalidValue;
+    if (p.scene.n_lds_prims > 0)
+      hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide3, kSceneLds, true>), dim3(blocks), dim3(threads), lds, stream, p);
+    else
+      hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide3, kNodesLds, true>), dim3(blocks), dim3(threads), lds, stream, p);
     return hipGetLastError();
   }
   switch (node_mode4(p.scene)) {

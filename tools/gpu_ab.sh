@@ -3,6 +3,7 @@
 # the headline bench: exp/<base> vs the in-tree build.  Usage: tools/gpu_ab.sh [base] [rounds]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ab
+export SHIRLEY_ASSETS=$PWD/shirley-raytracing-rs_amd/assets  # variant libs live in exp/<name>/
 base=${1:-base}; rounds=${2:-2}
 timeout -k 10 120 shirley-raytracing-rs_amd/bin/divcheck 24 8 || exit 1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -p no:cacheprovider tests/test_gpu_traversal.py tests/test_gpu_parity.py -k "traversal or render_matches or hit_queries or large_scene or edge or headline" > gpurun_out/ab/tests.log 2>&1
