@@ -1244,6 +1244,18 @@ __device__ __forceinline__ int select_lane(unsigned long long mask, int j) {
   }
   return lo;
 }
+// The inverse of the rank map of `mask`, for the whole wave in one forward permute: lane j (j <
+// popcount(mask)) receives the lane of mask's j-th set bit.  Every lane pushes its id (ds_permute:
+// dst[addr / 4] = src) — a set lane to slot rank, an unset lane to slot k + (its rank among the unset
+// lanes) — so the slots form a permutation and no two lanes write one slot.  Replaces a per-lane
+// binary search (select_lane, ~50 VALU) by a handful of instructions.  Wave-uniform control flow.
+__device__ __forceinline__ int rank_owners(unsigned long long mask) {
+  const int lane = __lane_id();
+  const int below = __popcll(mask & lanes_below());
+  const int k = __popcll(mask);
+  const int slot = ((mask >> lane) & 1ull) ? below : k + (lane - below);
+  return __builtin_amdgcn_ds_permute(slot << 2, lane);
+}
 
 // perlin/mod.rs:162-183 marble for every lane with `need`, computed by the whole wave: the k needing
 // lanes' 7 octaves are 7k work items (octave-major), dealt one per lane per round, so a wave needs
@@ -1259,13 +1271,14 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
   const int lane = __lane_id();
   const int rank = __popcll(mask & lanes_below());
   const int total = 7 * k;
+  const int owners = rank_owners(mask);  // lane j < k: the lane of the j-th needing lane
   double accum = 0.0;
   for (int base = 0; base < total; base += 64) {
     PH_COUNT(8);
     const int item = base + lane;
     const bool valid = item < total;
     const int oct = valid ? item / k : 0;
-    const int owner = select_lane(mask, valid ? item - oct * k : 0);
+    const int owner = __shfl(owners, valid ? item - oct * k : 0);
     const double qx = __shfl(p.x, owner), qy = __shfl(p.y, owner), qz = __shfl(p.z, owner);
     const int qt = __shfl(tab, owner);
     double nv = 0.0;
@@ -1336,7 +1349,7 @@ __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, 
     const int n = __popcll(mask);
     const int rank = __popcll(mask & lanes_below());  // meaningful for pending lanes
     const int q = lane % n, i = lane / n;
-    const int owner = select_lane(mask, q);
+    const int owner = __shfl(rank_owners(mask), q);
     const uint32_t t = (uint32_t)__shfl((int)r.draw, owner) + 3u * (uint32_t)i;
     const uint32_t pix = (uint32_t)__shfl((int)r.pixel, owner), smp = (uint32_t)__shfl((int)r.sample, owner);
     uint64_t a0, a1, b0, b1;
@@ -1373,6 +1386,152 @@ __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, 
     mask = __ballot(pending);
   }
   return p;
+}
+
+// All random draws of one megakernel iteration, by the whole wave at once.  A lane asks for one of:
+//   kDrawSphere — random_in_unit_sphere for its scatter (lambertian / metal / fairy light / isotropic),
+//                 draws d, d+1, d+2 per attempt (core/math.rs:32-45);
+//   kDrawDiel   — the dielectric's uniform (dielectric.rs:41), draw d — drawn speculatively: the
+//                 shader consumes it (advances the counter) only when there is no total internal
+//                 reflection, exactly like the reference's conditional draw;
+//   kDrawCam    — a new sample's camera draws: jitter x, y = draws 0, 1 (render.rs:60-63), then
+//                 random_in_unit_disk (camera/mod.rs:99-106, core/math.rs:70-81) from draw 2 on when
+//                 the camera has a lens, 2 draws per attempt.
+// First attempts: every lane's needs fit two Philox evaluations (block A, block B): a sphere attempt
+// at an even d takes blocks d/2 and d/2 + 1, at an odd d the cached odd half of block (d-1)/2 and block
+// (d+1)/2 = d/2 + 1; the dielectric's draw is block d/2's even half or the cache; the camera takes block
+// 0 (jitter) and block 1 (first disk attempt).  So two call sites serve the whole wave instead of
+// separate ones per material and a serial lens loop per new sample.  Rejected attempts (sphere or disk)
+// are then served together as in random_in_unit_sphere_coop: attempt i of the pending lane of rank q
+// runs on lane q + i n; a disk item evaluates two consecutive disk attempts (one per block).  Every
+// attempt is a pure function of (seed, pixel, sample, draw index), so the points, the draw counters and
+// the cached odd halves are exactly the serial loops'.  Must be called in wave-uniform control flow.
+// Returns: kDrawSphere -> the point; kDrawCam -> (disk x, disk y, 0) (lens) with the jitter in jx, jy;
+// kDrawDiel -> (uniform, bits of the cache after the draw, 0).
+enum : int { kDrawNone = 0, kDrawSphere = 1, kDrawDiel = 2, kDrawCam = 3 };
+__device__ __forceinline__ double u64_as_double(uint64_t v) { return __longlong_as_double((long long)v); }
+__device__ __forceinline__ uint64_t double_as_u64(double v) { return (uint64_t)__double_as_longlong(v); }
+__device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool lens, uint32_t pxy, double& jx,
+                                         double& jy) {
+  const bool cam = kind == kDrawCam;
+  const bool even = (r.draw & 1u) == 0u;
+  uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+  if (cam || ((kind == kDrawSphere || kind == kDrawDiel) && even))
+    philox_block(seed, r.pixel, r.sample, cam ? 0u : (r.draw >> 1), a0, a1);
+  if (kind == kDrawSphere || (cam && lens))
+    philox_block(seed, r.pixel, r.sample, cam ? 1u : (r.draw >> 1) + 1u, b0, b1);
+  const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
+  v3 p = V(0.0, 0.0, 0.0);
+  bool pending = false;
+  if (kind == kDrawSphere) {
+    const double x = -1.0 + (1.0 - -1.0) * unit_draw(even ? a0 : cached);  // random_real(-1, 1), same ops
+    const double y = -1.0 + (1.0 - -1.0) * unit_draw(even ? a1 : b0);
+    const double z = -1.0 + (1.0 - -1.0) * unit_draw(even ? b0 : b1);
+    r.draw += 3u;
+    r.c2 = (uint32_t)b1;  // the odd half of block d/2 + 1, as the serial draws leave it
+    r.c3 = (uint32_t)(b1 >> 32);
+    p = V(x, y, z);
+    pending = !(len2(p) <= 1.0);
+  } else if (kind == kDrawDiel) {
+    p = V(unit_draw(even ? a0 : cached), u64_as_double(even ? a1 : cached), 0.0);
+  } else if (cam) {
+    jx = (double)(pxy & 0xffffu) + unit_draw(a0);
+    jy = (double)(pxy >> 16) + unit_draw(a1);
+    r.draw = 2u;
+    if (lens) {
+      const double x = -1.0 + (1.0 - -1.0) * unit_draw(b0), y = -1.0 + (1.0 - -1.0) * unit_draw(b1);
+      p = V(x, y, 0.0);
+      r.draw = 4u;
+      pending = !(x * x + y * y <= 1.0);  // len2((x, y, 0)): the + 0*0 term cannot change a sum >= 0
+    }
+  }
+  unsigned long long mask = __ballot(pending);
+  if (mask == 0ull) return p;
+  const int lane = __lane_id();
+  const bool disk = cam;  // a pending camera lane is rejecting disk points
+  while (mask != 0ull) {
+    PH_COUNT(9);
+    const int n = __popcll(mask);
+    const int rank = __popcll(mask & lanes_below());  // meaningful for pending lanes
+    const int q = lane % n, i = lane / n;
+    const int owner = __shfl(rank_owners(mask), q);
+    const bool odisk = __shfl((int)disk, owner) != 0;
+    const uint32_t t0 = (uint32_t)__shfl((int)r.draw, owner);
+    const uint32_t pix = (uint32_t)__shfl((int)r.pixel, owner), smp = (uint32_t)__shfl((int)r.sample, owner);
+    // a sphere item is the attempt at draw t0 + 3i; a disk item the two attempts at draws t0 + 4i and
+    // t0 + 4i + 2 (t0 even), i.e. blocks t0/2 + 2i and t0/2 + 2i + 1
+    const uint32_t t = t0 + 3u * (uint32_t)i;
+    const uint32_t c = odisk ? (t0 >> 1) + 2u * (uint32_t)i : (t >> 1);
+    uint64_t e0, e1, f0, f1;
+    philox_block(seed, pix, smp, c, e0, e1);
+    philox_block(seed, pix, smp, c + 1u, f0, f1);
+    double x, y, z;
+    bool acc;
+    uint32_t used;  // draws this item consumed up to its accepted point (disk)
+    if (odisk) {
+      const double x1 = -1.0 + (1.0 - -1.0) * unit_draw(e0), y1 = -1.0 + (1.0 - -1.0) * unit_draw(e1);
+      const double x2 = -1.0 + (1.0 - -1.0) * unit_draw(f0), y2 = -1.0 + (1.0 - -1.0) * unit_draw(f1);
+      const bool acc1 = x1 * x1 + y1 * y1 <= 1.0;
+      acc = acc1 || x2 * x2 + y2 * y2 <= 1.0;
+      x = acc1 ? x1 : x2;
+      y = acc1 ? y1 : y2;
+      z = 0.0;
+      used = acc1 ? 2u : 4u;
+    } else {
+      const bool odd = (t & 1u) != 0u;
+      x = -1.0 + (1.0 - -1.0) * unit_draw(odd ? e1 : e0);
+      y = -1.0 + (1.0 - -1.0) * unit_draw(odd ? f0 : e1);
+      z = -1.0 + (1.0 - -1.0) * unit_draw(odd ? f1 : f0);
+      acc = len2(V(x, y, z)) <= 1.0;
+      used = 3u;
+    }
+    const unsigned long long accm = __ballot(acc);
+    // owners' first accepted item, level by level (wave-uniform masks of n bits)
+    const unsigned long long owners = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
+    unsigned long long found = 0ull;
+    int src = -1, lvl = 0;
+    for (int base = 0; base < 64 && found != owners; base += n, ++lvl) {
+      const unsigned long long bits = (accm >> base) & owners;
+      if (pending && ((bits & ~found) >> rank) & 1ull) src = lvl;
+      found |= bits;
+    }
+    const int sl = src >= 0 ? src * n + rank : 0;
+    const double sx = __shfl(x, sl), sy = __shfl(y, sl), sz = __shfl(z, sl);
+    const uint32_t s2 = (uint32_t)__shfl((int)(uint32_t)f1, sl), s3 = (uint32_t)__shfl((int)(uint32_t)(f1 >> 32), sl);
+    const uint32_t su = (uint32_t)__shfl((int)used, sl);
+    if (pending) {
+      const uint32_t stride = disk ? 4u : 3u;  // draws per item
+      if (src >= 0) {
+        p = V(sx, sy, sz);
+        r.draw += stride * (uint32_t)src + su;
+        r.c2 = s2;  // (a disk point leaves an even counter: the cache is then never read)
+        r.c3 = s3;
+        pending = false;
+      } else {
+        r.draw += stride * (uint32_t)((64 - rank + n - 1) / n);  // this round's items of this owner
+      }
+    }
+    mask = __ballot(pending);
+  }
+  return p;
+}
+
+// camera/mod.rs:97-132 from the sample's draws: jitter (x, y) and the unit-disk point (lens cameras)
+__device__ __forceinline__ void camera_ray_drawn(const DCamera& C, double x, double y, v3 disk, v3& o, v3& d) {
+  const double xp = x / (double)C.width;
+  const double yp = y / (double)C.height;
+  const v3 u = V(C.u[0], C.u[1], C.u[2]), v = V(C.v[0], C.v[1], C.v[2]);
+  const v3 origin = V(C.origin[0], C.origin[1], C.origin[2]);
+  v3 offset = V(0.0, 0.0, 0.0);
+  if (C.has_lens) {
+    const v3 rd = scale(disk, C.lens_radius);
+    offset = scale(u, rd.x) + scale(v, rd.y);
+  }
+  const v3 ll = V(C.lower_left[0], C.lower_left[1], C.lower_left[2]);
+  const v3 hz = V(C.horizontal[0], C.horizontal[1], C.horizontal[2]);
+  const v3 vt = V(C.vertical[0], C.vertical[1], C.vertical[2]);
+  d = (((ll + scale(hz, xp)) + scale(vt, yp)) - origin) - offset;
+  o = origin + offset;
 }
 
 // checker.rs:28-30
@@ -1578,6 +1737,9 @@ __device__ __forceinline__ bool shade(const DScene& S, const DPerlin* lds_perlin
 // computed by the wave (marble_coop, random_in_unit_sphere_coop), and `un` = the one unit vector the
 // material needs — unit(r) for lambertian / fairy light, unit(d) for dielectric / metal — computed
 // for all lanes at once instead of once per material branch.  Same steps otherwise.
+// DRAWN: the dielectric's uniform was drawn ahead by draws_coop (r = (uniform, bits of the cache after
+// it, 0)); it is consumed here — the counter advanced — only when the reference draws it (no TIR).
+template <bool DRAWN = false>
 __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, v3 r, v3 un,
                                           Rng& rng, uint64_t seed, v3& o, v3& d, const Hit& h, int prim,
                                           int face, v3& att, v3& em) {
@@ -1592,7 +1754,17 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
     double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
     bool refl = ratio * sin_theta > 1.0;
-    if (!refl) refl = reflectance(cos_theta, ratio) > rng_next(rng, seed);  // drawn only if not TIR
+    if (!refl) {  // drawn only if not TIR
+      if (DRAWN) {
+        refl = reflectance(cos_theta, ratio) > r.x;
+        const uint64_t cb = double_as_u64(r.y);
+        rng.draw += 1u;
+        rng.c2 = (uint32_t)cb;
+        rng.c3 = (uint32_t)(cb >> 32);
+      } else {
+        refl = reflectance(cos_theta, ratio) > rng_next(rng, seed);
+      }
+    }
     o = h.point;
     d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
     return true;  // attenuation = Color::ones()

@@ -89,20 +89,76 @@ void trace_kernel(KParams P) {
 #ifdef RT_PHASE_TIMING
   unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
 #endif
+  // One iteration: (1) a ray_color segment for every lane holding a path (closest hit, record,
+  // material); (2) lanes whose path ends here (sky or a light) or that hold none take the next sample
+  // of their unit or a new unit; (3) one wave-wide sampler draws everything the iteration needs — the
+  // scatters' unit-sphere points, the dielectrics' uniforms and the new samples' jitter + lens points;
+  // (4) shading; ended lanes add their radiance and publish finished units; new samples' camera rays.
   for (;;) {
+#ifdef RT_PHASE_TIMING
+    const unsigned long long ph1 = clock64();
+    const unsigned long long ph_before = ph_lane_steps;
+#endif
+    // 1. one ray_color iteration (render.rs:30-46): closest hit and hit record, the material and the
+    // texture leaf of a diffuse / emitting material
+    bool hit = false, need_pn = false, need_r = false;
+    int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0, mk = -1;
+    double t_best = __builtin_inf(), psc = 0.0;
+    Hit h;
+    h.point = V(0.0, 0.0, 0.0);
+    h.normal = h.point;
+    h.t = h.u = h.v = 0.0;
+    h.front_face = false;
+#ifdef RT_PHASE_TIMING
+    unsigned long long ph2 = ph1;
+#endif
+    PH_COUNT(6);
+    n_seg += __popcll(__ballot(active));
+    if (active) {
+#ifdef RT_PHASE_TIMING
+      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits, ptests,
+                                      ph_lane_steps);
+      ph2 = clock64();
+      ph_trav += ph2 - ph1;
+#else
+      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
+                                      ptests);
+#endif
+      if (prim >= 0) {
+        hit = true;
+        const DPrim pr = S.prims[prim];
+        hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
+        mat = pr.material;
+        mk = S.mats[mat].kind;
+        need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
+        if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
+          leaf = resolve_texture(S, S.mats[mat].tex, h.point);
+          const DTex& tx = S.texs[leaf];
+          if (tx.kind == RT_TEX_PERLIN) {
+            need_pn = true;
+            ptab = tx.table;
+            psc = tx.scale;
+          }
+        }
+      }
+    }
 #ifdef RT_PHASE_TIMING
     const unsigned long long ph0 = clock64();
 #endif
-    // 1. a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
-    if (has_unit && !active && rng.sample + 1u >= (uint32_t)s_end) {
-      double* dst = P.partial + (size_t)part_index * 3;
-      dst[0] = sum.x;
-      dst[1] = sum.y;
-      dst[2] = sum.z;
+    // 2. the path ends at this segment when it misses (the sky) or meets a material that does not
+    // scatter (diffuse light): known before shading, so the lane's next sample starts in this iteration
+    const bool ends = active && (!hit || mk == RT_MAT_DIFFUSE_LIGHT);
+    const bool free_lane = !active || ends;
+    // a unit whose last sample ends here is published after shading (its sum is complete then)
+    bool publish = false;
+    uint32_t pub_index = 0;
+    if (free_lane && has_unit && rng.sample + 1u >= (uint32_t)s_end) {
+      publish = true;
+      pub_index = part_index;
       has_unit = false;
     }
-    // 2. idle lanes take units from the wave's window (one global atomic per 64 units)
-    bool need = !has_unit;
+    // lanes without a unit take one from the wave's window (one global atomic per 64 units)
+    bool need = free_lane && !has_unit;
     unsigned long long mask = __ballot(need);
     if (mask != 0ull && !exhausted) {
       unsigned long long k = __popcll(mask);
@@ -146,95 +202,41 @@ void trace_kernel(KParams P) {
           rng.pixel = (uint32_t)py * (uint32_t)C.width + (uint32_t)px;
           pxy = (uint32_t)px | ((uint32_t)py << 16);
           part_index = (uint32_t)chunk * pix_per_chunk + lt * (uint32_t)kTilePixels + (uint32_t)lp;
-          sum = V(0.0, 0.0, 0.0);
         }
       }
     }
-    // 3. lanes between paths start the next sample (render.rs:60-65)
-    const bool start = has_unit && !active && rng.sample + 1u < (uint32_t)s_end;
-    n_samp += __popcll(__ballot(start));
-    if (start) {
+    // a free lane holding a unit starts its next sample (render.rs:60-65): draws from 0 again
+    const bool regen = free_lane && has_unit;
+    n_samp += __popcll(__ballot(regen));
+    if (regen) {
       rng.sample += 1u;
       rng.draw = 0;
-      double jx = (double)(pxy & 0xffffu) + rng_next(rng, seed);
-      double jy = (double)(pxy >> 16) + rng_next(rng, seed);
-      camera_ray(C, rng, seed, jx, jy, o, d);
-      att = V(1.0, 1.0, 1.0);
-      em = V(0.0, 0.0, 0.0);
-      depth_left = W.max_depth;
-      active = depth_left > 0;
-      if (!active) sum = sum + em;  // max_depth == 0: ray_color returns black (render.rs:30)
     }
-    if (!__any(active)) {
-      // with max_depth > 0 a lane holding a unit is active here (a unit whose last sample ended
-      // was published in step 1, a new or continuing one started a sample in step 3), so no lane
-      // holds a unit once none is active and the pool is drained.  max_depth == 0 (no path ever
-      // becomes active) never reaches this kernel: render_window writes its black frame itself.
-      if (exhausted) break;
-      continue;
-    }
-    // 4. one ray_color iteration (render.rs:30-46): closest hit, then emitted + scatter or sky
 #ifdef RT_PHASE_TIMING
-    const unsigned long long ph1 = clock64();
-    ph_regen += ph1 - ph0;
-    const unsigned long long ph_before = ph_lane_steps;
+    const unsigned long long ph3 = clock64();
+    ph_regen += ph3 - ph0;
 #endif
-    // (a) closest hit, hit record, and the texture leaf of a diffuse / emitting material
-    bool hit = false, need_pn = false, need_r = false;
-    int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0, mk = -1;
-    double t_best = __builtin_inf(), psc = 0.0;
-    Hit h;
-    h.point = V(0.0, 0.0, 0.0);
-    h.normal = h.point;
-    h.t = h.u = h.v = 0.0;
-    h.front_face = false;
-#ifdef RT_PHASE_TIMING
-    unsigned long long ph2 = ph1;
-#endif
-    PH_COUNT(6);
-    n_seg += __popcll(__ballot(active));
-    if (active) {
-#ifdef RT_PHASE_TIMING
-      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits, ptests,
-                                      ph_lane_steps);
-      ph2 = clock64();
-      ph_trav += ph2 - ph1;
-#else
-      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
-                                      ptests);
-#endif
-      if (prim >= 0) {
-        hit = true;
-        const DPrim pr = S.prims[prim];
-        hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
-        mat = pr.material;
-        mk = S.mats[mat].kind;
-        need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
-        if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
-          leaf = resolve_texture(S, S.mats[mat].tex, h.point);
-          const DTex& tx = S.texs[leaf];
-          if (tx.kind == RT_TEX_PERLIN) {
-            need_pn = true;
-            ptab = tx.table;
-            psc = tx.scale;
-          }
-        }
-      }
-    }
-    // (b) Perlin marble values for the lanes that need one, by the whole wave (wave-uniform)
+    // 3. Perlin marble values for the lanes that need one, by the whole wave (wave-uniform)
     const double pn = lds_perlin ? marble_coop((LdsPerlin*)lds_perlin, need_pn, ptab, psc, h.point)
                                  : marble_coop(S.perlin, need_pn, ptab, psc, h.point);
-    // (b') the scatter's random_in_unit_sphere for the lanes whose material draws one, by the wave
-    const v3 rs = random_in_unit_sphere_coop(rng, seed, need_r);
-    // (b'') the one normalisation a lane's shading needs, for all lanes at once: unit(r) for a
-    // lambertian / fairy light hit, unit(d) for dielectric, metal and the sky (idle lanes: a dummy)
-    const v3 un = unit_fast(!active ? V(1.0, 1.0, 1.0) : (need_r && mk != RT_MAT_METAL) ? rs : d);
-    // (c) emitted + scatter (render.rs:31-45) or the sky
+    // every draw of the iteration, by the wave: the scatter's random_in_unit_sphere, the dielectric's
+    // uniform, a new sample's jitter and lens point
+    const bool scat = active && !ends;
+    const int dk = regen ? kDrawCam
+                         : (scat && need_r) ? kDrawSphere : (scat && mk == RT_MAT_DIELECTRIC) ? kDrawDiel : kDrawNone;
+    double jx = 0.0, jy = 0.0;
+    const v3 rs = draws_coop(rng, seed, dk, C.has_lens != 0, pxy, jx, jy);
+    // the one normalisation a lane's shading needs, for all lanes at once: unit(r) for a lambertian /
+    // fairy light scatter, unit(d) for dielectric, metal and the sky (others: a dummy)
+    const v3 un = unit_fast(!active ? V(1.0, 1.0, 1.0) : (scat && need_r && mk != RT_MAT_METAL) ? rs : d);
+    // 4. emitted + scatter (render.rs:31-45) or the sky; an ended lane's o, d are free once un holds
+    // unit(d), so its new sample's camera ray is formed first
+    if (regen) camera_ray_drawn(C, jx, jy, rs, o, d);
     if (active) {
       bool alive;
       if (hit) {
         const DMat m = S.mats[mat];
-        alive = shade_pre(S, m, leaf, pn, rs, un, rng, seed, o, d, h, prim, face, att, em);
+        alive = shade_pre<true>(S, m, leaf, pn, rs, un, rng, seed, o, d, h, prim, face, att, em);
       } else {
         em = em + hmul(att, sky_unit(S, un));
         alive = false;
@@ -244,10 +246,27 @@ void trace_kernel(KParams P) {
         sum = sum + em;  // c += ray_color(...)
         active = false;
       }
-#ifdef RT_PHASE_TIMING
-      ph_shade += clock64() - ph2;
-#endif
     }
+    // a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
+    if (publish) {
+      double* dst = P.partial + (size_t)pub_index * 3;
+      dst[0] = sum.x;
+      dst[1] = sum.y;
+      dst[2] = sum.z;
+      sum = V(0.0, 0.0, 0.0);
+    }
+    if (regen) {
+      att = V(1.0, 1.0, 1.0);
+      em = V(0.0, 0.0, 0.0);
+      depth_left = W.max_depth;  // >= 1: max_depth == 0 frames are written by render_window itself
+      active = true;
+    }
+#ifdef RT_PHASE_TIMING
+    ph_shade += clock64() - ph3;
+#endif
+    // done when no lane holds a path or a unit and the pool is drained (a lane that fails to get a
+    // unit while the pool is not drained — e.g. an edge tile's unit outside the image — retries)
+    if (exhausted && !__any(active || has_unit)) break;
 #ifdef RT_PHASE_TIMING
     {
       unsigned dl = (unsigned)(ph_lane_steps - ph_before);  // this lane's steps (0 when idle)

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 tag=${1:-r01}; shift
-args=${@:---steps 2 --warmup 1 --no-cpu}
+args=${@:---steps 2 --warmup 1 --no-cpu --no-configs}
 out=gpurun_out/prof_$tag
 mkdir -p $out
 set -o pipefail

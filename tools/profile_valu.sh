@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 tag=${1:-r02}; shift
 out=gpurun_out/valu_$tag
 mkdir -p $out
-args="--spp 50 --steps 1 --warmup 0 --no-cpu --bvh sah $@"
+args="--spp 50 --steps 1 --warmup 0 --no-cpu --no-configs --bvh sah $@"
 i=0
 for set in "SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_SALU"; do
   i=$((i+1))
