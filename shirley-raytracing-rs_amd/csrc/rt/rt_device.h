@@ -743,7 +743,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
 // per-lane step counter of the instrumented build (a register of the calling kernel)
 #define g_trav_lane_steps trav_lane_steps_ref
 // event counters of the instrumented build: slot 2i += active lanes, slot 2i + 1 += 1 (per wave)
-static __device__ unsigned long long g_phase_ctr[32];
+static __device__ unsigned long long g_phase_ctr[64];
 __device__ __forceinline__ void ph_count(int i) {
   const unsigned long long act = __ballot(1);
   if ((int)__lane_id() == __builtin_ctzll(act)) {
@@ -884,8 +884,14 @@ __device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
   const int lo = (k & 1) ? c1 : c0, hi = (k & 1) ? c3 : c2;
   return (k & 2) ? hi : lo;
 }
-// f32 upper bound of a t: rounded up, and finite so that a +inf key (a miss) never passes `k <= tmaxf`
-__device__ __forceinline__ float tmax_f32(double t) { return fminf(__double2float_ru(t), 3.402823466e38f); }
+// f32 upper bound of a t, finite so that a +inf key (a miss) never passes `k <= tmaxf`.  f = (float)t
+// rounds to nearest, so |t - f| <= ulp(f) / 2, and f + |f| 2^-23 >= f + ulp(f) (toward +inf for either
+// sign) is >= t after its own rounding: four instructions instead of the emulated round-up conversion
+// (~20).  The bound may be up to two f32 ulps above t: a few more subtrees kept, never one dropped.
+__device__ __forceinline__ float tmax_f32(double t) {
+  const float f = (float)t;
+  return fminf(f + fabsf(f) * 0x1p-23f, 3.402823466e38f);
+}
 // The top bytes of four words as one word, byte i = w_i >> 24 (two v_perm_b32 and an or).  Leaf
 // masks are kept in this "spread" form: bit 8 i + 7 stands for child i.
 __device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned w2, unsigned w3) {
@@ -1056,6 +1062,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
                                          , unsigned long long& trav_lane_steps_ref
 #endif
                                          ) {
+  PH_COUNT(23);
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   const RaySigns ns = ray_signs(inv);
   const RayF rf = ray_f(S, o, inv);
@@ -1298,6 +1305,7 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
     }
   }
   const double turb = 10.0 * fabs(accum);
+  if (need) PH_COUNT(14);
   return need ? 0.5 * (1.0 + sin(sc * p.z + turb)) : 0.0;
 }
 
@@ -1402,8 +1410,8 @@ __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, 
 // (d+1)/2 = d/2 + 1; the dielectric's draw is block d/2's even half or the cache; the camera takes block
 // 0 (jitter) and block 1 (first disk attempt).  So two call sites serve the whole wave instead of
 // separate ones per material and a serial lens loop per new sample.  Rejected attempts (sphere or disk)
-// are then served together as in random_in_unit_sphere_coop: attempt i of the pending lane of rank q
-// runs on lane q + i n; a disk item evaluates two consecutive disk attempts (one per block).  Every
+// are then served together as in random_in_unit_sphere_coop, each pending lane getting a block of
+// consecutive lanes per round; a disk item evaluates two consecutive disk attempts (one per block).  Every
 // attempt is a pure function of (seed, pixel, sample, draw index), so the points, the draw counters and
 // the cached odd halves are exactly the serial loops'.  Must be called in wave-uniform control flow.
 // Returns: kDrawSphere -> the point; kDrawCam -> (disk x, disk y, 0) (lens) with the jitter in jx, jy;
@@ -1416,30 +1424,38 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
   const bool cam = kind == kDrawCam;
   const bool even = (r.draw & 1u) == 0u;
   uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-  if (cam || ((kind == kDrawSphere || kind == kDrawDiel) && even))
+  if (cam || ((kind == kDrawSphere || kind == kDrawDiel) && even)) {
+    PH_COUNT(12);
     philox_block(seed, r.pixel, r.sample, cam ? 0u : (r.draw >> 1), a0, a1);
-  if (kind == kDrawSphere || (cam && lens))
+  }
+  if (kind == kDrawSphere || (cam && lens)) {
+    PH_COUNT(13);
     philox_block(seed, r.pixel, r.sample, cam ? 1u : (r.draw >> 1) + 1u, b0, b1);
+  }
   const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
+  // the first attempts' uniforms, converted once for every kind: a sphere takes u0 u1 u2 (x y z), a
+  // camera u0 u1 (jitter) and u2 u3 (disk), a dielectric u0
+  const bool sph = kind == kDrawSphere;
+  const double u0 = unit_draw((!even && !cam) ? cached : a0);
+  const double u1 = unit_draw((sph && !even) ? b0 : a1);
+  const double u2 = unit_draw((sph && !even) ? b1 : b0);
+  const double u3 = unit_draw(b1);
   v3 p = V(0.0, 0.0, 0.0);
   bool pending = false;
-  if (kind == kDrawSphere) {
-    const double x = -1.0 + (1.0 - -1.0) * unit_draw(even ? a0 : cached);  // random_real(-1, 1), same ops
-    const double y = -1.0 + (1.0 - -1.0) * unit_draw(even ? a1 : b0);
-    const double z = -1.0 + (1.0 - -1.0) * unit_draw(even ? b0 : b1);
+  if (sph) {
+    p = V(-1.0 + (1.0 - -1.0) * u0, -1.0 + (1.0 - -1.0) * u1, -1.0 + (1.0 - -1.0) * u2);  // random_real(-1, 1)
     r.draw += 3u;
     r.c2 = (uint32_t)b1;  // the odd half of block d/2 + 1, as the serial draws leave it
     r.c3 = (uint32_t)(b1 >> 32);
-    p = V(x, y, z);
     pending = !(len2(p) <= 1.0);
   } else if (kind == kDrawDiel) {
-    p = V(unit_draw(even ? a0 : cached), u64_as_double(even ? a1 : cached), 0.0);
+    p = V(u0, u64_as_double(even ? a1 : cached), 0.0);
   } else if (cam) {
-    jx = (double)(pxy & 0xffffu) + unit_draw(a0);
-    jy = (double)(pxy >> 16) + unit_draw(a1);
+    jx = (double)(pxy & 0xffffu) + u0;
+    jy = (double)(pxy >> 16) + u1;
     r.draw = 2u;
     if (lens) {
-      const double x = -1.0 + (1.0 - -1.0) * unit_draw(b0), y = -1.0 + (1.0 - -1.0) * unit_draw(b1);
+      const double x = -1.0 + (1.0 - -1.0) * u2, y = -1.0 + (1.0 - -1.0) * u3;
       p = V(x, y, 0.0);
       r.draw = 4u;
       pending = !(x * x + y * y <= 1.0);  // len2((x, y, 0)): the + 0*0 term cannot change a sum >= 0
@@ -1448,15 +1464,24 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
   unsigned long long mask = __ballot(pending);
   if (mask == 0ull) return p;
   const int lane = __lane_id();
-  const bool disk = cam;  // a pending camera lane is rejecting disk points
+  // a pending camera lane rejects disk points; the flag rides in bit 31 of the shared draw counter
+  const uint32_t disk_bit = cam ? 0x80000000u : 0u;
   while (mask != 0ull) {
     PH_COUNT(9);
+    // the n pending lanes get m = 64 / n consecutive items each: owner q's items are lanes [q m, q m + m)
+    // (the 64 - n m others idle), so an owner's first accepted item is the lowest set bit of an m-bit
+    // field of the acceptance ballot
     const int n = __popcll(mask);
+    const int m = 64 / n;
     const int rank = __popcll(mask & lanes_below());  // meaningful for pending lanes
-    const int q = lane % n, i = lane / n;
-    const int owner = __shfl(rank_owners(mask), q);
-    const bool odisk = __shfl((int)disk, owner) != 0;
-    const uint32_t t0 = (uint32_t)__shfl((int)r.draw, owner);
+    // q = lane / m exactly: (lane + 1/2) / m stays >= 1 / (2m) >= 2^-7 away from an integer
+    const int q = (int)(((float)lane + 0.5f) * __builtin_amdgcn_rcpf((float)m));
+    const int i = lane - q * m;
+    const bool valid = q < n;
+    const int owner = __shfl(rank_owners(mask), valid ? q : 0);
+    const uint32_t tw = (uint32_t)__shfl((int)(r.draw | disk_bit), owner);
+    const bool odisk = (tw & 0x80000000u) != 0u;
+    const uint32_t t0 = tw & 0x7fffffffu;
     const uint32_t pix = (uint32_t)__shfl((int)r.pixel, owner), smp = (uint32_t)__shfl((int)r.sample, owner);
     // a sphere item is the attempt at draw t0 + 3i; a disk item the two attempts at draws t0 + 4i and
     // t0 + 4i + 2 (t0 even), i.e. blocks t0/2 + 2i and t0/2 + 2i + 1
@@ -1465,42 +1490,36 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
     uint64_t e0, e1, f0, f1;
     philox_block(seed, pix, smp, c, e0, e1);
     philox_block(seed, pix, smp, c + 1u, f0, f1);
+    const double d0 = -1.0 + (1.0 - -1.0) * unit_draw(e0), d1 = -1.0 + (1.0 - -1.0) * unit_draw(e1);
+    const double d2 = -1.0 + (1.0 - -1.0) * unit_draw(f0), d3 = -1.0 + (1.0 - -1.0) * unit_draw(f1);
     double x, y, z;
     bool acc;
     uint32_t used;  // draws this item consumed up to its accepted point (disk)
     if (odisk) {
-      const double x1 = -1.0 + (1.0 - -1.0) * unit_draw(e0), y1 = -1.0 + (1.0 - -1.0) * unit_draw(e1);
-      const double x2 = -1.0 + (1.0 - -1.0) * unit_draw(f0), y2 = -1.0 + (1.0 - -1.0) * unit_draw(f1);
-      const bool acc1 = x1 * x1 + y1 * y1 <= 1.0;
-      acc = acc1 || x2 * x2 + y2 * y2 <= 1.0;
-      x = acc1 ? x1 : x2;
-      y = acc1 ? y1 : y2;
+      const bool acc1 = d0 * d0 + d1 * d1 <= 1.0;
+      acc = acc1 || d2 * d2 + d3 * d3 <= 1.0;
+      x = acc1 ? d0 : d2;
+      y = acc1 ? d1 : d3;
       z = 0.0;
       used = acc1 ? 2u : 4u;
     } else {
       const bool odd = (t & 1u) != 0u;
-      x = -1.0 + (1.0 - -1.0) * unit_draw(odd ? e1 : e0);
-      y = -1.0 + (1.0 - -1.0) * unit_draw(odd ? f0 : e1);
-      z = -1.0 + (1.0 - -1.0) * unit_draw(odd ? f1 : f0);
+      x = odd ? d1 : d0;
+      y = odd ? d2 : d1;
+      z = odd ? d3 : d2;
       acc = len2(V(x, y, z)) <= 1.0;
       used = 3u;
     }
-    const unsigned long long accm = __ballot(acc);
-    // owners' first accepted item, level by level (wave-uniform masks of n bits)
-    const unsigned long long owners = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
-    unsigned long long found = 0ull;
-    int src = -1, lvl = 0;
-    for (int base = 0; base < 64 && found != owners; base += n, ++lvl) {
-      const unsigned long long bits = (accm >> base) & owners;
-      if (pending && ((bits & ~found) >> rank) & 1ull) src = lvl;
-      found |= bits;
-    }
-    const int sl = src >= 0 ? src * n + rank : 0;
+    const unsigned long long accm = __ballot(valid && acc);
+    const int shift = pending ? rank * m : 0;  // < 64 for a pending lane (rank < n, n m <= 64)
+    const unsigned long long field = (m == 64 ? accm : (accm >> shift) & ((1ull << m) - 1ull));
+    const int src = (pending && field != 0ull) ? (int)__builtin_ctzll(field) : -1;
+    const int sl = src >= 0 ? rank * m + src : 0;
     const double sx = __shfl(x, sl), sy = __shfl(y, sl), sz = __shfl(z, sl);
     const uint32_t s2 = (uint32_t)__shfl((int)(uint32_t)f1, sl), s3 = (uint32_t)__shfl((int)(uint32_t)(f1 >> 32), sl);
     const uint32_t su = (uint32_t)__shfl((int)used, sl);
     if (pending) {
-      const uint32_t stride = disk ? 4u : 3u;  // draws per item
+      const uint32_t stride = disk_bit ? 4u : 3u;  // draws per item
       if (src >= 0) {
         p = V(sx, sy, sz);
         r.draw += stride * (uint32_t)src + su;
@@ -1508,7 +1527,7 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
         r.c3 = s3;
         pending = false;
       } else {
-        r.draw += stride * (uint32_t)((64 - rank + n - 1) / n);  // this round's items of this owner
+        r.draw += stride * (uint32_t)m;  // this round's items of this owner
       }
     }
     mask = __ballot(pending);
@@ -1573,6 +1592,7 @@ __device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
   for (;;) {
     const DTex& t = S.texs[ti];
     if (t.kind != RT_TEX_CHECKER) return ti;
+    PH_COUNT(16);
     ti = checker_odd(t.scale, p.x, p.y, p.z) ? t.odd : t.even;
   }
 }
@@ -1744,17 +1764,20 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
                                           Rng& rng, uint64_t seed, v3& o, v3& d, const Hit& h, int prim,
                                           int face, v3& att, v3& em) {
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
+    PH_COUNT(21);
     v3 e = leaf_texture_value(S, leaf, pn, prim, face, h);
     em = em + hmul(att, e);
     return false;
   }
   if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
+    PH_COUNT(17);
     double ratio = h.front_face ? (1.0 / m.param) : m.param;
     const v3 ud = un;
     double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
     double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
     bool refl = ratio * sin_theta > 1.0;
     if (!refl) {  // drawn only if not TIR
+      PH_COUNT(22);
       if (DRAWN) {
         refl = reflectance(cos_theta, ratio) > r.x;
         const uint64_t cb = double_as_u64(r.y);
@@ -1770,6 +1793,7 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     return true;  // attenuation = Color::ones()
   }
   if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
+    PH_COUNT(18);
     v3 reflected = reflect(un, h.normal);
     o = h.point;
     d = reflected + scale(r, m.param);
@@ -1783,6 +1807,7 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     return true;
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
+  PH_COUNT(19);
   v3 a = leaf_texture_value(S, leaf, pn, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
     double s = dot(h.normal, scale(d, -1.0));

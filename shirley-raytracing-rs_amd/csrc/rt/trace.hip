@@ -125,6 +125,7 @@ void trace_kernel(KParams P) {
                                       ptests);
 #endif
       if (prim >= 0) {
+        PH_COUNT(15);
         hit = true;
         const DPrim pr = S.prims[prim];
         hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
@@ -195,6 +196,7 @@ void trace_kernel(KParams P) {
         const int px = tx * kTile + (lp % kTile);
         const int py = ty * kTile + (lp / kTile);
         if (px < C.width && py < C.height) {
+          PH_COUNT(10);
           has_unit = true;
           const int s0 = chunk * W.chunk;
           s_end = min(W.samples, s0 + W.chunk);
@@ -231,13 +233,17 @@ void trace_kernel(KParams P) {
     const v3 un = unit_fast(!active ? V(1.0, 1.0, 1.0) : (scat && need_r && mk != RT_MAT_METAL) ? rs : d);
     // 4. emitted + scatter (render.rs:31-45) or the sky; an ended lane's o, d are free once un holds
     // unit(d), so its new sample's camera ray is formed first
-    if (regen) camera_ray_drawn(C, jx, jy, rs, o, d);
+    if (regen) {
+      PH_COUNT(11);
+      camera_ray_drawn(C, jx, jy, rs, o, d);
+    }
     if (active) {
       bool alive;
       if (hit) {
         const DMat m = S.mats[mat];
         alive = shade_pre<true>(S, m, leaf, pn, rs, un, rng, seed, o, d, h, prim, face, att, em);
       } else {
+        PH_COUNT(20);
         em = em + hmul(att, sky_unit(S, un));
         alive = false;
       }
@@ -249,6 +255,7 @@ void trace_kernel(KParams P) {
     }
     // a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
     if (publish) {
+      PH_COUNT(24);
       double* dst = P.partial + (size_t)pub_index * 3;
       dst[0] = sum.x;
       dst[1] = sum.y;
@@ -628,15 +635,18 @@ hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, 
 #ifdef RT_PHASE_TIMING
 // instrumented build: print and clear the event counters (slot 2i: lane events, 2i + 1: wave events)
 void phase_counters_dump() {
-  unsigned long long h[32];
+  unsigned long long h[64];
   if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_phase_ctr), sizeof h) != hipSuccess) return;
   static const char* names[] = {"visit", "visit_with_leaves", "sphere_iter", "sphere_slab_pass", "rect_iter",
-                                "pop_iter", "segment_iter", "box_iter", "marble_round", "sphere_coop_round"};
-  for (int i = 0; i < 10; ++i)
+                                "pop_iter", "segment_iter", "box_iter", "marble_round", "draws_coop_round",
+                                "unit_fetch", "camera_ray", "philox_A", "philox_B", "marble_sin", "hit_record",
+                                "checker_level", "dielectric", "metal", "lambertian", "sky", "diffuse_light",
+                                "reflectance", "traverse4", "publish"};
+  for (int i = 0; i < 25; ++i)
     if (h[2 * i + 1])
       fprintf(stderr, "[phase-ev] %-18s lanes %.4g waves %.4g lanes/wave %.2f\n", names[i], (double)h[2 * i],
               (double)h[2 * i + 1], (double)h[2 * i] / (double)h[2 * i + 1]);
-  unsigned long long z[32] = {};
+  unsigned long long z[64] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_ctr), z, sizeof z);
 }
 #endif
