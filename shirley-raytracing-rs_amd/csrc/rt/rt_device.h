@@ -1264,12 +1264,19 @@ __device__ __forceinline__ int rank_owners(unsigned long long mask) {
   return __builtin_amdgcn_ds_permute(slot << 2, lane);
 }
 
-// perlin/mod.rs:162-183 marble for every lane with `need`, computed by the whole wave: the k needing
-// lanes' 7 octaves are 7k work items (octave-major), dealt one per lane per round, so a wave needs
-// ceil(7k / 64) noise evaluations instead of 7 (the octave loop otherwise runs for all lanes while
-// any one needs it).  Octave i's input p * 2^i is the reference's tp after i doublings (scaling by 2 is
-// exact), its weight 0.5^i likewise, and each owner adds its octaves in the reference's order — the
-// value is bit-identical.  Must be called in wave-uniform control flow (it shuffles).
+// v from lane L - 1 on lane L (lane 0: 0), a whole-wave DPP shift (wave_shr:1) of both halves
+__device__ __forceinline__ double lane_shift_up(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+// perlin/mod.rs:162-183 marble for every lane with `need`, computed by the whole wave: a round serves
+// 9 needing lanes, needing lane j's 7 octaves being lanes 7j .. 7j + 6, so a wave needs ceil(k / 9)
+// noise evaluations instead of 7 (the octave loop otherwise runs for all lanes while any one needs
+// it).  Octave i's input p * 2^i is the reference's tp after i doublings (scaling by 2 is exact), its
+// weight 0.5^i likewise; the octaves are then summed in the reference's order along the 7 lanes (six
+// one-lane DPP shifts of the running sums) — the value is bit-identical.  Must be called in wave-uniform control flow (it shuffles).
 template <class TP>
 __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, double sc, v3 p) {
   const unsigned long long mask = __ballot(need);
@@ -1277,15 +1284,14 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
   const int k = __popcll(mask);
   const int lane = __lane_id();
   const int rank = __popcll(mask & lanes_below());
-  const int total = 7 * k;
   const int owners = rank_owners(mask);  // lane j < k: the lane of the j-th needing lane
+  const int jl = lane / 7, oct = lane - 7 * jl;
+  const double w = __builtin_amdgcn_ldexp(1.0, -oct);  // the reference's weight after oct halvings
   double accum = 0.0;
-  for (int base = 0; base < total; base += 64) {
+  for (int base = 0; base < k; base += 9) {
     PH_COUNT(8);
-    const int item = base + lane;
-    const bool valid = item < total;
-    const int oct = valid ? item / k : 0;
-    const int owner = __shfl(owners, valid ? item - oct * k : 0);
+    const bool valid = lane < 63 && base + jl < k;
+    const int owner = __shfl(owners, valid ? base + jl : 0);
     const double qx = __shfl(p.x, owner), qy = __shfl(p.y, owner), qz = __shfl(p.z, owner);
     const int qt = __shfl(tab, owner);
     double nv = 0.0;
@@ -1293,16 +1299,16 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
       const double f = (double)(1 << oct);  // 2^oct, exact
       nv = perlin_noise_t(tables + qt, V(qx * f, qy * f, qz * f));
     }
-    // owners take their octaves of this round, in octave order
-    double w = 1.0;
+    // accum = 0.0; accum += weight * noise, in octave order.  Every lane adds what the lane below held
+    // one step earlier, so at step s lane 7j + s holds octaves 0 .. s of lane j (by induction: it read
+    // lane 7j + s - 1 after step s - 1); what the other lanes hold then is never read.
+    const double term = w * nv;
+    double run = 0.0 + term;
 #pragma unroll
-    for (int i = 0; i < 7; ++i) {
-      const int my = i * k + rank;
-      const bool mine = need && my >= base && my < base + 64;
-      const double v = __shfl(nv, mine ? my - base : 0);
-      if (mine) accum += w * v;
-      w *= 0.5;
-    }
+    for (int st = 1; st < 7; ++st) run = lane_shift_up(run) + term;
+    const bool mine = need && rank >= base && rank < base + 9;
+    const double v = __shfl(run, mine ? 7 * (rank - base) + 6 : 0);
+    if (mine) accum = v;
   }
   const double turb = 10.0 * fabs(accum);
   if (need) PH_COUNT(14);
