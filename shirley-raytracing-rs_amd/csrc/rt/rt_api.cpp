@@ -839,6 +839,8 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   kp.work.max_depth = p->max_depth;
   kp.work.seed = p->seed;
   kp.work.n_units = (uint64_t)n_pix * (uint64_t)n_chunks;
+  kp.work.div_unit_tile = make_udiv((uint32_t)n_chunks * (uint32_t)kTilePixels);
+  kp.work.div_tiles_x = make_udiv((uint32_t)L.tiles_x);
   kp.partial = static_cast<double*>(c->partial.p);
   kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
   kp.counters = static_cast<DCounters*>(c->counters.p);
@@ -1013,6 +1015,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     q.tex = m.texture;
     for (int k = 0; k < 3; ++k) q.albedo[k] = m.albedo[k];
     q.param = m.param;
+    q.inv_param = 1.0 / m.param;  // IEEE division: the bits dielectric.rs:27 computes per hit
   }
   std::vector<DTex> texs(std::max(1, d->n_textures));
   for (int i = 0; i < d->n_textures; ++i) {

@@ -94,7 +94,7 @@ __device__ __forceinline__ double fmin_one(double x) { return (x < 1.0) ? x : 1.
 __device__ __forceinline__ v3 refract(v3 uv, v3 n, double eta) {
   double cos_theta = fmin_one(dot(scale(uv, -1.0), n));
   v3 r_out_perp = scale(scale(n, cos_theta) + uv, eta);
-  double r_out_parallel_mag = sqrt(fabs(1.0 - len2(r_out_perp))) * -1.0;
+  double r_out_parallel_mag = sqrt_rn(fabs(1.0 - len2(r_out_perp))) * -1.0;
   return r_out_perp + scale(n, r_out_parallel_mag);
 }
 
@@ -105,6 +105,11 @@ __device__ __forceinline__ v3 refract(v3 uv, v3 n, double eta) {
 struct Rng {
   uint32_t pixel, sample, draw, c2, c3;
 };
+// n / d with the launch's UDiv of d (rt_layout.h make_udiv)
+__device__ __forceinline__ uint32_t udiv(uint32_t n, const UDiv& D) {
+  const uint32_t t = __umulhi(D.m, n);
+  return (t + ((n - t) >> D.s1)) >> D.s2;
+}
 // a ^ b ^ c in one instruction (gfx950 v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -1777,10 +1782,10 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
   }
   if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
     PH_COUNT(17);
-    double ratio = h.front_face ? (1.0 / m.param) : m.param;
+    double ratio = h.front_face ? m.inv_param : m.param;  // 1.0 / ir, precomputed
     const v3 ud = un;
     double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
-    double sin_theta = sqrt(1.0 - cos_theta * cos_theta);
+    double sin_theta = sqrt_rn(1.0 - cos_theta * cos_theta);
     bool refl = ratio * sin_theta > 1.0;
     if (!refl) {  // drawn only if not TIR
       PH_COUNT(22);

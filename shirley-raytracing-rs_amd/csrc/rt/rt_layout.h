@@ -91,7 +91,7 @@ struct alignas(16) DMat {
   int32_t tex;
   double albedo[3];
   double param;
-  double pad;
+  double inv_param;  // 1.0 / param, computed on the host (the dielectric's front-face ratio 1.0 / ir)
 };
 static_assert(sizeof(DMat) == 48, "DMat layout");
 
@@ -152,7 +152,24 @@ struct DCamera {
 };
 
 // Work decomposition: unit = (local tile, sample chunk, lane) ; see trace.hip.
+// Unsigned 32-bit division by a divisor fixed for a launch (Granlund & Montgomery 1994, "Division by
+// invariant integers using multiplication", Fig. 4.1): q = (t + ((n - t) >> s1)) >> s2 with
+// t = mulhi(m, n), l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, s1 = min(l, 1), s2 = max(l - 1, 0);
+// exact for every 32-bit n.  Built on the host, applied per lane in a few instructions instead of a
+// generic division sequence.
+struct UDiv {
+  uint32_t m, s1, s2;
+};
+inline UDiv make_udiv(uint32_t d) {
+  uint32_t l = 0;
+  while (l < 32 && (1ull << l) < d) ++l;
+  const uint64_t m = (((1ull << l) - d) << 32) / d + 1;
+  return UDiv{(uint32_t)m, l < 1 ? l : 1u, l > 0 ? l - 1 : 0u};
+}
+
 struct DWork {
+  UDiv div_unit_tile;            // / (n_chunks * kTilePixels): unit index -> the rank's local tile
+  UDiv div_tiles_x;              // / tiles_x
   int32_t tiles_x, tiles_y;      // tile grid of the rendered window (tiles_y rows from ty0)
   int32_t tile_rank, tile_world;
   int32_t n_tiles_rank;          // tiles owned by this rank

@@ -185,9 +185,9 @@ void trace_kernel(KParams P) {
         // unit -> (local tile, chunk, lane-in-tile); tile-major so a window = 64 neighbours.  32-bit
         // quotients (the host keeps n_units < 2^32): far cheaper than 64-bit ones
         const uint32_t pt = (uint32_t)W.n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
-        const uint32_t lt = i32 / pt;
+        const uint32_t lt = udiv(i32, W.div_unit_tile);  // i32 / pt
         const uint32_t g32 = lt * (uint32_t)W.tile_world + (uint32_t)W.tile_rank;
-        const uint32_t y32 = g32 / (uint32_t)W.tiles_x;
+        const uint32_t y32 = udiv(g32, W.div_tiles_x);  // g32 / tiles_x
         const uint32_t rem = i32 - lt * pt;
         const int tx = (int)(g32 - y32 * (uint32_t)W.tiles_x);
         const int ty = W.ty0 + (int)y32;
