@@ -1833,6 +1833,70 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
   return true;
 }
 
+// shade_pre<true> with the path's attenuation and emission left to the caller, so that the megakernel
+// reads and writes them once per segment instead of once per material branch: the material's
+// attenuation factor goes to `mul` (att = att * mul; 1 for a dielectric, exact) and its emission to
+// `emit` with `has_emit` (em = em + att * emit, applied before the factor — the reference's order for
+// the fairy light).  Same arithmetic as shade_pre.
+__device__ __forceinline__ bool shade_factor(const DScene& S, const DMat& m, int leaf, double pn, v3 r, v3 un,
+                                             Rng& rng, v3& o, v3& d, const Hit& h, int prim, int face, v3& mul,
+                                             v3& emit, bool& has_emit) {
+  if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
+    PH_COUNT(21);
+    emit = leaf_texture_value(S, leaf, pn, prim, face, h);
+    has_emit = true;
+    return false;
+  }
+  if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
+    PH_COUNT(17);
+    double ratio = h.front_face ? m.inv_param : m.param;  // 1.0 / ir, precomputed
+    const v3 ud = un;
+    double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
+    double sin_theta = sqrt_rn(1.0 - cos_theta * cos_theta);
+    bool refl = ratio * sin_theta > 1.0;
+    if (!refl) {  // drawn only if not TIR: the uniform drawn ahead by draws_coop is consumed
+      PH_COUNT(22);
+      refl = reflectance(cos_theta, ratio) > r.x;
+      const uint64_t cb = double_as_u64(r.y);
+      rng.draw += 1u;
+      rng.c2 = (uint32_t)cb;
+      rng.c3 = (uint32_t)(cb >> 32);
+    }
+    o = h.point;
+    d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
+    return true;  // attenuation = Color::ones()
+  }
+  if (m.kind == RT_MAT_METAL) {  // metal.rs:26-40 — never absorbs
+    PH_COUNT(18);
+    v3 reflected = reflect(un, h.normal);
+    o = h.point;
+    d = reflected + scale(r, m.param);
+    mul = V(m.albedo[0], m.albedo[1], m.albedo[2]);
+    return true;
+  }
+  if (m.kind == RT_MAT_ISOTROPIC) {  // book-2 isotropic (extension): random_in_unit_sphere, albedo
+    mul = leaf_texture_value(S, leaf, pn, prim, face, h);
+    o = h.point;
+    d = r;
+    return true;
+  }
+  // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
+  PH_COUNT(19);
+  v3 a = leaf_texture_value(S, leaf, pn, prim, face, h);
+  if (m.kind == RT_MAT_FAIRY_LIGHT) {
+    double s = dot(h.normal, scale(d, -1.0));
+    emit = scale(a, s / len(d));
+    has_emit = true;
+    a = unit(a);
+  }
+  v3 sc = h.normal + un;
+  if (near_zero(sc)) sc = h.normal;
+  o = h.point;
+  d = sc;
+  mul = a;
+  return true;
+}
+
 // camera/mod.rs:97-132 (horizontal / vertical / lower_left precomputed on the host, same ops)
 __device__ __forceinline__ void camera_ray(const DCamera& C, Rng& rng, uint64_t seed, double x, double y, v3& o,
                                            v3& d) {

@@ -238,15 +238,20 @@ void trace_kernel(KParams P) {
       camera_ray_drawn(C, jx, jy, rs, o, d);
     }
     if (active) {
-      bool alive;
+      bool alive, has_emit = false;
+      v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
       if (hit) {
         const DMat m = S.mats[mat];
-        alive = shade_pre<true>(S, m, leaf, pn, rs, un, rng, seed, o, d, h, prim, face, att, em);
+        alive = shade_factor(S, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
       } else {
         PH_COUNT(20);
-        em = em + hmul(att, sky_unit(S, un));
+        emit = sky_unit(S, un);
+        has_emit = true;
         alive = false;
       }
+      // the path's throughput and radiance, read and written once per segment
+      if (has_emit) em = em + hmul(att, emit);
+      att = hmul(att, mul);
       if (alive) alive = --depth_left > 0;
       if (!alive) {
         sum = sum + em;  // c += ray_color(...)
