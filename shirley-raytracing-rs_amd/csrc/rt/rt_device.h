@@ -749,6 +749,8 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
 #define g_trav_lane_steps trav_lane_steps_ref
 // event counters of the instrumented build: slot 2i += active lanes, slot 2i + 1 += 1 (per wave)
 static __device__ unsigned long long g_phase_ctr[64];
+// histograms of the instrumented build: node visits per traversing lane, and per wave (its slowest lane)
+static __device__ unsigned long long g_visit_hist[64], g_wave_visit_hist[64];
 __device__ __forceinline__ void ph_count(int i) {
   const unsigned long long act = __ballot(1);
   if ((int)__lane_id() == __builtin_ctzll(act)) {

@@ -282,8 +282,10 @@ void trace_kernel(KParams P) {
 #ifdef RT_PHASE_TIMING
     {
       unsigned dl = (unsigned)(ph_lane_steps - ph_before);  // this lane's steps (0 when idle)
+      if (dl > 0) atomicAdd(&g_visit_hist[min(dl, 63u)], 1ull);
       for (int off = 32; off > 0; off >>= 1) dl = max(dl, (unsigned)__shfl_xor((int)dl, off));
       ph_wave_steps += dl;  // the wave's loop iterations = its slowest lane's steps
+      if (lane == 0 && dl > 0) atomicAdd(&g_wave_visit_hist[min(dl, 63u)], 1ull);
     }
 #endif
     if (visits > (1u << 30) || ptests > (1u << 30)) {  // (never within a frame of today's sizes)
@@ -651,8 +653,17 @@ void phase_counters_dump() {
     if (h[2 * i + 1])
       fprintf(stderr, "[phase-ev] %-18s lanes %.4g waves %.4g lanes/wave %.2f\n", names[i], (double)h[2 * i],
               (double)h[2 * i + 1], (double)h[2 * i] / (double)h[2 * i + 1]);
+  unsigned long long lh[64], wh[64];
+  if (hipMemcpyFromSymbol(lh, HIP_SYMBOL(g_visit_hist), sizeof lh) == hipSuccess &&
+      hipMemcpyFromSymbol(wh, HIP_SYMBOL(g_wave_visit_hist), sizeof wh) == hipSuccess) {
+    fprintf(stderr, "[phase-hist] visits: lanes / waves (slowest lane)\n");
+    for (int i = 1; i < 64; ++i)
+      if (lh[i] || wh[i]) fprintf(stderr, "[phase-hist] %2d %.6g %.6g\n", i, (double)lh[i], (double)wh[i]);
+  }
   unsigned long long z[64] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_ctr), z, sizeof z);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_visit_hist), z, sizeof z);
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_visit_hist), z, sizeof z);
 }
 #endif
 

@@ -7,7 +7,7 @@
 
 #define CHAINS 8
 template <int OP>
-__global__ __launch_bounds__(768) void kern(int n, unsigned long long* out, unsigned* sink) {
+__global__ __launch_bounds__(1024) void kern(int n, unsigned long long* out, unsigned* sink) {
   unsigned a[CHAINS];
   double f[CHAINS];
   unsigned long long w[CHAINS];
