@@ -986,6 +986,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
              : o.geometry == RT_GEOM_RECT_XZ  ? kPrimRectXZ
              : o.geometry == RT_GEOM_RECT_BOX ? kPrimBox
                                               : kPrimMovingSphere;
+    // a sphere's 1 / radius (sphere.rs:48 `scale(1.0 / self.radius)`), the same IEEE quotient the device
+    // would compute per hit record; p[4] is otherwise unused by spheres
+    if (q.kind == kPrimSphere || q.kind == kPrimMovingSphere) q.p[4] = 1.0 / q.p[3];
     q.material = o.material;
     if (is_extended(o)) {
       if (exts.size() >= (1u << (31 - kPrimExtShift)))

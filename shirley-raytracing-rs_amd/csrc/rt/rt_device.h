@@ -503,7 +503,7 @@ __device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 
   double u = 0.0, v = 0.0;
   if (pr.kind == kPrimSphere) {
     // sphere.rs:46-51 + get_uv 17-26: u, v from the outward normal (p - c) / r (signed r)
-    normal = scale(h.point - V(pr.p[0], pr.p[1], pr.p[2]), 1.0 / pr.p[3]);
+    normal = scale(h.point - V(pr.p[0], pr.p[1], pr.p[2]), pr.p[4]);  // p[4] = 1.0 / r (host)
     if (WANT_UV) {
       UV uv = sphere_uv(normal.x, normal.y, normal.z);
       u = uv.u;
@@ -555,7 +555,7 @@ __device__ __forceinline__ Hit ext_record(const DExt* exts, double time0, double
     const v3 c = moving_center(pr, e, ray_time(time0, time1, pixel, sample, seed));
     h.t = t;
     h.point = o + scale(d, t);
-    const v3 n = scale(h.point - c, 1.0 / pr.p[3]);
+    const v3 n = scale(h.point - c, pr.p[4]);  // p[4] = 1.0 / r (host)
     const UV uv = sphere_uv(n.x, n.y, n.z);
     h.u = uv.u;
     h.v = uv.v;

@@ -80,7 +80,7 @@ static_assert(sizeof(DExt) == 144, "DExt layout");
 
 // One primitive = one reference leaf object (a RectBox stays ONE leaf of 6 faces, rect.rs:146-156).
 struct alignas(16) DPrim {
-  double p[6];       // sphere: cx cy cz r ; rect: d1_min d1_max d2_min d2_max offset ; box: min xyz max xyz
+  double p[6];       // sphere: cx cy cz r 1/r ; rect: d1_min d1_max d2_min d2_max offset ; box: min xyz max xyz
   int32_t kind;
   int32_t material;
 };
