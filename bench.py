@@ -303,8 +303,9 @@ def main():
                    "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
                                        "texture": round(laps[-1][5], 3)} if args.timing else None,
                    "segments_per_sample": round(seg / max(float(np.mean(samples)), 1.0), 4),
-                   "node_tests_per_segment": round(laps[-1][6] / max(seg, 1), 3),
-                   "prim_tests_per_segment": round(laps[-1][7] / max(seg, 1), 3)},
+                   # counted by the instrumented build only (RT_PHASE_TIMING): null here
+                   "node_tests_per_segment": round(laps[-1][6] / max(seg, 1), 3) if laps[-1][6] else None,
+                   "prim_tests_per_segment": round(laps[-1][7] / max(seg, 1), 3) if laps[-1][7] else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),

@@ -762,6 +762,13 @@ __device__ __forceinline__ void ph_count(int i) {
 #else
 #define PH_COUNT(i)
 #endif
+// Per-lane node-visit / primitive-test statistics of the 4-wide traversal: counted in the instrumented
+// build only (they cost the production megakernel 0.5 %: ~15 VALU per iteration and two registers).
+#ifdef RT_PHASE_TIMING
+#define RT_STAT(x) x
+#else
+#define RT_STAT(x)
+#endif
 template <int MODE>
 __device__ __forceinline__ const DNode4F& fetch_node4(const DScene& S, const DNode4F* lds_nodes, int idx) {
   // LDS byte offset with a full-rate 24-bit multiply (an LDS node index is < 2^24)
@@ -926,7 +933,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
     double t;
     PH_COUNT(3);
-    ++ptests;
+    RT_STAT(++ptests);
     if (sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
 #pragma unroll 1
@@ -939,7 +946,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double b[6], te, t;
     leaf_box(pr, b);
     if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
-    ++ptests;
+    RT_STAT(++ptests);
     bool h;
     switch (pr.kind) {
       case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t); break;
@@ -958,13 +965,13 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double te, t;
     if (EXT && pr.kind != kPrimBox) {  // an extended primitive (book 2): exact box from its DExt record
       if (!slab_s(prim_ext(S, pr).box, o, inv, ns, t_min, t_best, te)) continue;
-      ++ptests;
+      RT_STAT(++ptests);
       int f = -1;
       if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
       continue;
     }
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
-    ++ptests;
+    RT_STAT(++ptests);
     const int f = box_t(pr.p, o, d, t_min, t_best, t);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
@@ -998,7 +1005,7 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* 
   ch = *reinterpret_cast<const int4*>(nd.child);
   const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
   node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
-  visits += 4;
+  RT_STAT(visits += 4);
   // hit leaf: key < inf (bits(k) + 0x80800000 keeps the sign bit exactly for bits(k) < bits(inf); keys
   // are >= 0) and a negative child word; as a spread mask
   const unsigned h0 = (__float_as_uint(k0) + 0x80800000u) & (unsigned)ch.x;
