@@ -2,8 +2,7 @@
 # Build an experiment variant of libshirley_rt.so into exp/<name>/ (for tools/ab2.sh).
 # Usage: tools/variant.sh <name> [extra hipcc flags...]   e.g. tools/variant.sh phase -DRT_PHASE_TIMING
 # The tree is copied, so a variant can also be made from edited sources: set SRC=<dir> (default: the
-# in-tree package).  LICM_FLAG= / TRK_FLAG= (empty) build without
-# -disable-machine-licm / -amdgpu-use-amdgpu-trackers.
+# in-tree package).  LICM_FLAG= (empty) builds without -disable-machine-licm; TRK_FLAG=<flags> adds scheduler flags.
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift
@@ -14,7 +13,7 @@ cp -r "$src"/csrc "$src"/Makefile "$tmp"/
 mkdir -p "$tmp/../include" 2>/dev/null || true
 cp -r include "$tmp/../" 2>/dev/null || true
 make -C "$tmp" -j8 lib/libshirley_rt.so \
-  HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function ${LICM_FLAG--mllvm -disable-machine-licm} ${TRK_FLAG--mllvm -amdgpu-use-amdgpu-trackers=1} $*" >/dev/null
+  HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function ${LICM_FLAG--mllvm -disable-machine-licm} ${TRK_FLAG-} $*" >/dev/null
 mkdir -p exp/$name
 cp "$tmp/lib/libshirley_rt.so" exp/$name/
 cp shirley-raytracing-rs_amd/lib/libshirley_host.so exp/$name/
