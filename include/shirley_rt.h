@@ -192,8 +192,10 @@ typedef struct rt_scene_stats {
 typedef struct rt_counters {
   uint64_t samples;     /* paths started = pixels x spp */
   uint64_t segments;    /* ray_color loop iterations that traced a ray (hit + miss) */
-  uint64_t node_visits; /* BVH child-box tests (4-wide trees: 4 per node visit) */
-  uint64_t prim_tests;  /* primitive intersection calls */
+  uint64_t node_visits; /* BVH child-box tests (4-wide trees: 4 per node visit); the 4-wide traversal of the
+                         * megakernel / wavefront counts them only in the instrumented build (-DRT_PHASE_TIMING,
+                         * DESIGN.md §5): 0 otherwise */
+  uint64_t prim_tests;  /* primitive intersection calls (same condition) */
   double kernel_ms;     /* device time of the trace (all trace kernels of the frame, HIP events) */
   double reduce_ms;     /* device time of the partial-sum reduce kernel */
   int32_t engine;       /* RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT or RT_ENGINE_SPLIT: the engine that ran */
