@@ -86,7 +86,7 @@ struct rt_ctx {
   bool has_perlin = false;
   int n_perlin = 0;
   // per-render scratch
-  DevBuf partial, accum, counters, unit_counter;
+  DevBuf partial, accum, counters, unit_counter, kcam;
   DevBuf wf_pool, wf_iters;          // path slots (SoA) + texture queue; per-iteration counters ring
   uint32_t* wf_host = nullptr;       // pinned readback of the retired-slot count, one word per batch
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -845,6 +845,10 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
   kp.counters = static_cast<DCounters*>(c->counters.p);
 
+  st = ensure(c, c->kcam, sizeof(DCamera));
+  if (st) return st;
+  HIP_TRY(c, hipMemcpyAsync(c->kcam.p, &kp.cam, sizeof(DCamera), hipMemcpyHostToDevice, s));
+  kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
   HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
   HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
   c->last_engine = engine;
@@ -937,7 +941,7 @@ int rt_destroy(rt_ctx* c) {
   if (!c) return RT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->exts, &c->partial,
+  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->exts, &c->partial, &c->kcam,
                     &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters, &c->packed, &c->gathered})
     release(*b);
   for (rt_comm& m : c->group_comms)

@@ -198,6 +198,9 @@ struct KParams {
   unsigned long long* unit_counter;  // work-queue head (one 64-unit batch per fetch)
   DCounters* counters;
   int32_t split_refill;          // split_kernel: idle traversal lanes before a wave claims rays (>= 1)
+  // device copy of `cam` (megakernel): read with scalar loads where a new sample's camera ray is
+  // formed instead of being held in SGPRs across the whole loop (where it spills to VGPR lanes)
+  uint64_t cam_const;
 };
 
 // ---- wavefront engine (wavefront.hip): path state of P slots as structure-of-arrays in HBM ----

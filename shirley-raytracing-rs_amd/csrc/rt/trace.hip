@@ -235,7 +235,11 @@ void trace_kernel(KParams P) {
     // unit(d), so its new sample's camera ray is formed first
     if (regen) {
       PH_COUNT(11);
-      camera_ray_drawn(C, jx, jy, rs, o, d);
+      // the camera read with scalar loads here (an opaque copy of its address keeps them from being
+      // hoisted): held in SGPRs across the loop it spills to VGPR lanes, ~66 v_readlane per iteration
+      KCamera* kc = (KCamera*)(uintptr_t)P.cam_const;
+      asm volatile("" : "+s"(kc));
+      camera_ray_drawn(*kc, jx, jy, rs, o, d);
     }
     if (active) {
       bool alive, has_emit = false;
