@@ -845,10 +845,14 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
   kp.counters = static_cast<DCounters*>(c->counters.p);
 
-  st = ensure(c, c->kcam, sizeof(DCamera));
+  // device copies of the camera and the work descriptor (KParams.cam_const / work_const)
+  st = ensure(c, c->kcam, 2 * sizeof(DCamera) + sizeof(DWork));
   if (st) return st;
   HIP_TRY(c, hipMemcpyAsync(c->kcam.p, &kp.cam, sizeof(DCamera), hipMemcpyHostToDevice, s));
+  void* kwork = static_cast<char*>(c->kcam.p) + 2 * sizeof(DCamera);  // (16-B aligned)
+  HIP_TRY(c, hipMemcpyAsync(kwork, &kp.work, sizeof(DWork), hipMemcpyHostToDevice, s));
   kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
+  kp.work_const = (uint64_t)(uintptr_t)kwork;
   HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
   HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
   c->last_engine = engine;

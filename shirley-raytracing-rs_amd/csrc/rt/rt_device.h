@@ -1558,6 +1558,7 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
 // camera/mod.rs:97-132 from the sample's draws: jitter (x, y) and the unit-disk point (lens cameras).
 // CAM: a DCamera (reference) or a pointer-like to one (the megakernel's constant-address-space copy).
 typedef __attribute__((address_space(4))) const DCamera KCamera;
+typedef __attribute__((address_space(4))) const DWork KWork;
 template <class CAM>
 __device__ __forceinline__ void camera_ray_drawn(const CAM& C, double x, double y, v3 disk, v3& o, v3& d) {
   const double xp = x / (double)C.width;

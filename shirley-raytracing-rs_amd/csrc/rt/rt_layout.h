@@ -201,6 +201,7 @@ struct KParams {
   // device copy of `cam` (megakernel): read with scalar loads where a new sample's camera ray is
   // formed instead of being held in SGPRs across the whole loop (where it spills to VGPR lanes)
   uint64_t cam_const;
+  uint64_t work_const;           // device copy of `work`, read the same way where a unit is taken
 };
 
 // ---- wavefront engine (wavefront.hip): path state of P slots as structure-of-arrays in HBM ----

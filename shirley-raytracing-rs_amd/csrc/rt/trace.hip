@@ -84,7 +84,6 @@ void trace_kernel(KParams P) {
   Rng rng{0, 0, 0, 0, 0};
   unsigned long long n_seg = 0, n_samp = 0;  // wave-uniform (SGPRs): popcounts of ballots
   unsigned visits = 0, ptests = 0;           // per lane; flushed to the counters before 2^31
-  const uint32_t pix_per_chunk = (uint32_t)W.n_tiles_rank * (uint32_t)kTilePixels;
 
 #ifdef RT_PHASE_TIMING
   unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
@@ -183,27 +182,32 @@ void trace_kernel(KParams P) {
       }
       if (need && idx < W.n_units) {
         // unit -> (local tile, chunk, lane-in-tile); tile-major so a window = 64 neighbours.  32-bit
-        // quotients (the host keeps n_units < 2^32): far cheaper than 64-bit ones
-        const uint32_t pt = (uint32_t)W.n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
-        const uint32_t lt = udiv(i32, W.div_unit_tile);  // i32 / pt
-        const uint32_t g32 = lt * (uint32_t)W.tile_world + (uint32_t)W.tile_rank;
-        const uint32_t y32 = udiv(g32, W.div_tiles_x);  // g32 / tiles_x
+        // quotients (the host keeps n_units < 2^32): far cheaper than 64-bit ones.  The work
+        // descriptor and the image size are read here with scalar loads, like the camera below.
+        KWork* kw = (KWork*)(uintptr_t)P.work_const;
+        KCamera* kc = (KCamera*)(uintptr_t)P.cam_const;
+        asm volatile("" : "+s"(kw), "+s"(kc));
+        const uint32_t pt = (uint32_t)kw->n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
+        const uint32_t lt = udiv(i32, UDiv{kw->div_unit_tile.m, kw->div_unit_tile.s1, kw->div_unit_tile.s2});  // i32 / pt
+        const uint32_t g32 = lt * (uint32_t)kw->tile_world + (uint32_t)kw->tile_rank;
+        const uint32_t y32 = udiv(g32, UDiv{kw->div_tiles_x.m, kw->div_tiles_x.s1, kw->div_tiles_x.s2});  // g32 / tiles_x
         const uint32_t rem = i32 - lt * pt;
-        const int tx = (int)(g32 - y32 * (uint32_t)W.tiles_x);
-        const int ty = W.ty0 + (int)y32;
+        const int tx = (int)(g32 - y32 * (uint32_t)kw->tiles_x);
+        const int ty = kw->ty0 + (int)y32;
         int chunk = (int)(rem / kTilePixels);
         int lp = (int)(rem % kTilePixels);
         const int px = tx * kTile + (lp % kTile);
         const int py = ty * kTile + (lp / kTile);
-        if (px < C.width && py < C.height) {
+        if (px < kc->width && py < kc->height) {
           PH_COUNT(10);
           has_unit = true;
-          const int s0 = chunk * W.chunk;
-          s_end = min(W.samples, s0 + W.chunk);
+          const int s0 = chunk * kw->chunk;
+          s_end = min(kw->samples, s0 + kw->chunk);
           rng.sample = (uint32_t)s0 - 1u;  // advanced before each sample (wraps to s0)
-          rng.pixel = (uint32_t)py * (uint32_t)C.width + (uint32_t)px;
+          rng.pixel = (uint32_t)py * (uint32_t)kc->width + (uint32_t)px;
           pxy = (uint32_t)px | ((uint32_t)py << 16);
-          part_index = (uint32_t)chunk * pix_per_chunk + lt * (uint32_t)kTilePixels + (uint32_t)lp;
+          part_index = (uint32_t)chunk * ((uint32_t)kw->n_tiles_rank * (uint32_t)kTilePixels) +
+                       lt * (uint32_t)kTilePixels + (uint32_t)lp;
         }
       }
     }
