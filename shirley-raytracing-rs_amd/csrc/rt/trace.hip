@@ -126,7 +126,7 @@ void trace_kernel(KParams P) {
       if (prim >= 0) {
         PH_COUNT(15);
         hit = true;
-        const DPrim pr = S.prims[prim];
+        const DPrim pr = (MODE == kSceneLds) ? lds_prims[prim] : S.prims[prim];  // (LDS copy when resident)
         hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
         mat = pr.material;
         mk = S.mats[mat].kind;
