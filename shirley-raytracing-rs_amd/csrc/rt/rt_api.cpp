@@ -20,7 +20,8 @@
 #include "rt_layout.h"
 
 namespace rt {
-size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads);
+size_t trace_lds_bytes(int n_lds_nodes4, int node4_size, int n_lds_prims, int n_lds_perlin, int stack_depth4,
+                       int threads);
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
 bool split_supported_nt(int nt);
@@ -406,16 +407,20 @@ Inflation inflation_for(const BuiltTree& t) {
 // NaN plane always passes (its leaf is tested exactly anyway)
 void set_child_box(DNode4F& n, int slot, const Box* b, double delta) {
   for (int a = 0; a < 3; ++a) {
+    float lo, hi;
     if (!b) {
-      n.lo[a][slot] = INFINITY;
-      n.hi[a][slot] = -INFINITY;
+      lo = INFINITY;
+      hi = -INFINITY;
     } else if (std::isnan(b->mn[a]) || std::isnan(b->mx[a])) {
-      n.lo[a][slot] = -INFINITY;
-      n.hi[a][slot] = INFINITY;
+      lo = -INFINITY;
+      hi = INFINITY;
     } else {
-      n.lo[a][slot] = round_down(b->mn[a] - delta);
-      n.hi[a][slot] = round_up(b->mx[a] + delta);
+      lo = round_down(b->mn[a] - delta);
+      hi = round_up(b->mx[a] + delta);
     }
+    n.row[a][0][slot] = lo;
+    n.row[a][1][slot] = hi;
+    n.row[a][2][slot] = lo;
   }
 }
 
@@ -1059,7 +1064,22 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   if (texels.empty()) texels.resize(16);
 
   if ((st = upload(c, c->nodes, nodes.data(), nodes.size() * sizeof(DNode)))) return st;
-  if ((st = upload(c, c->nodes4, nodes4.data(), nodes4.size() * sizeof(DNode4F)))) return st;
+  // book-2 scenes run the EXT kernel instances, which read the compact node layout (rt_layout.h)
+  const int n4_bytes = node4_bytes(!exts.empty());
+  if (exts.empty()) {
+    if ((st = upload(c, c->nodes4, nodes4.data(), nodes4.size() * sizeof(DNode4F)))) return st;
+  } else {
+    std::vector<DNode4C> compact(nodes4.size());
+    for (size_t i = 0; i < nodes4.size(); ++i) {
+      for (int a = 0; a < 3; ++a)
+        for (int k = 0; k < 4; ++k) {
+          compact[i].lo[a][k] = nodes4[i].row[a][0][k];
+          compact[i].hi[a][k] = nodes4[i].row[a][1][k];
+        }
+      for (int k = 0; k < 4; ++k) compact[i].child[k] = nodes4[i].child[k];
+    }
+    if ((st = upload(c, c->nodes4, compact.data(), compact.size() * sizeof(DNode4C)))) return st;
+  }
   if ((st = upload(c, c->prims, prims.data(), prims.size() * sizeof(DPrim)))) return st;
   if ((st = upload(c, c->mats, mats.data(), mats.size() * sizeof(DMat)))) return st;
   if ((st = upload(c, c->texs, texs.data(), texs.size() * sizeof(DTex)))) return st;
@@ -1074,7 +1094,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
 
   DScene& S = c->scene;
   S.nodes = static_cast<const DNode*>(c->nodes.p);
-  S.nodes4 = static_cast<const DNode4F*>(c->nodes4.p);
+  S.nodes4 = c->nodes4.p;
   S.n_nodes4 = (int32_t)nodes4.size();
   S.stack_depth4 = stack4;
   S.root4 = (nodes4[0].child[0] >= 0 && nodes4[0].child[0] != kEmptyChild) ? nodes4[0].child[0] : 0;
@@ -1113,18 +1133,19 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   auto lds_nodes_for = [&](long long stack) { return lds_count(stack, sizeof(DNode), nodes.size()); };
   const long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
   const long long stack4_bytes = (long long)S.stack_depth4 * kTraceThreads * kStack4EntryBytes;
+  // book-2 scenes: the EXT instance spills ~80 VGPRs at 4 waves per SIMD (1024 threads) and none at 3
+  // (768 threads, 165 VGPRs): final_scene +3.3 % (profiles/r02/wide3.txt).  SHIRLEY_WIDE4: tuning switch.
+  // The wide block's LDS holds the tree plus one stack per thread of the block actually launched.
+  const int wide_threads = (!exts.empty() && !getenv("SHIRLEY_WIDE4")) ? kTraceThreadsWide3 : kTraceThreadsWide;
   const long long wide_bytes =
-      (long long)S.stack_depth4 * kTraceThreadsWide * kStack4EntryBytes + (long long)nodes4.size() * sizeof(DNode4F);
+      (long long)S.stack_depth4 * wide_threads * kStack4EntryBytes + (long long)nodes4.size() * n4_bytes;
   if (stack_bytes > kLdsBytes || stack4_bytes > kLdsBytes)
     return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
   const bool wide = wide_bytes <= kLdsBytes && (placement == 0 || placement == RT_BVH_NODES_LDS) &&
                     !getenv("SHIRLEY_NO_WIDE");  // tuning
-  c->mk_threads = wide ? kTraceThreadsWide : kTraceThreads;
-  // book-2 scenes: the EXT instance spills ~80 VGPRs at 4 waves per SIMD (1024 threads) and none at 3
-  // (768 threads, 165 VGPRs): final_scene +3.3 % (profiles/r02/wide3.txt).  SHIRLEY_WIDE4: tuning switch.
-  if (wide && !exts.empty() && !getenv("SHIRLEY_WIDE4")) c->mk_threads = kTraceThreadsWide3;
+  c->mk_threads = wide ? wide_threads : kTraceThreads;
   S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
-  S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, sizeof(DNode4F), nodes4.size());
+  S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, n4_bytes, nodes4.size());
   // primitives too, when they fit beside the wide block's tree and stacks (leaf tests from LDS)
   const bool prims_lds = wide && wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) <= kLdsBytes &&
                          !getenv("SHIRLEY_NO_LDS_PRIMS");

@@ -769,22 +769,24 @@ __device__ __forceinline__ void ph_count(int i) {
 #else
 #define RT_STAT(x)
 #endif
-template <int MODE>
-__device__ __forceinline__ const DNode4F& fetch_node4(const DScene& S, const DNode4F* lds_nodes, int idx) {
+template <int MODE, class N4>
+__device__ __forceinline__ const N4& fetch_node4(const DScene& S, const N4* lds_nodes, int idx) {
   // LDS byte offset with a full-rate 24-bit multiply (an LDS node index is < 2^24)
   if (MODE == kNodesLds || MODE == kSceneLds)
-    return *reinterpret_cast<const DNode4F*>(reinterpret_cast<const char*>(lds_nodes) +
-                                             __umul24((unsigned)idx, (unsigned)sizeof(DNode4F)));
-  if (MODE == kNodesGlobal) return S.nodes4[idx];
-  return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : S.nodes4[idx];
+    return *reinterpret_cast<const N4*>(reinterpret_cast<const char*>(lds_nodes) +
+                                        __umul24((unsigned)idx, (unsigned)sizeof(N4)));
+  const N4* g = static_cast<const N4*>(S.nodes4);
+  if (MODE == kNodesGlobal) return g[idx];
+  return (idx < S.n_lds_nodes4) ? lds_nodes[idx] : g[idx];
 }
 
 // Ray in the form the f32 node test uses: o and 1/d rounded to f32, and o * (1/d) for the FMA.
 struct RayF {
   float ox, oy, oz, ix, iy, iz, oix, oiy, oiz;
   bool fast;  // max|o| <= origin_limit: the f32 test's error bound holds
-  int dx, dy, dz;  // 48 when 1/d < 0 on the axis (the near plane is the hi row of DNode4F), else 0
+  int dx, dy, dz;  // N4::kNegRow when 1/d < 0 on the axis (the near plane is the hi row), else 0
 };
+template <class N4>
 __device__ __forceinline__ RayF ray_f(const DScene& S, v3 o, v3 inv) {
   RayF r;
   r.ox = (float)o.x;
@@ -797,9 +799,9 @@ __device__ __forceinline__ RayF ray_f(const DScene& S, v3 o, v3 inv) {
   r.oiy = r.oy * r.iy;
   r.oiz = r.oz * r.iz;
   r.fast = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z)) <= (double)S.origin_limit;
-  r.dx = r.ix < 0.f ? 48 : 0;
-  r.dy = r.iy < 0.f ? 48 : 0;
-  r.dz = r.iz < 0.f ? 48 : 0;
+  r.dx = r.ix < 0.f ? N4::kNegRow : 0;
+  r.dy = r.iy < 0.f ? N4::kNegRow : 0;
+  r.dz = r.iz < 0.f ? N4::kNegRow : 0;
   return r;
 }
 
@@ -812,20 +814,33 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 f2(float a, float b) { return f32x2{a, b}; }
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-__device__ __forceinline__ void node4_keys(const DNode4F& nd, const RayF& r, v3 o, v3 inv, float tminf, float tmaxf,
+template <class N4>
+__device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3 inv, float tminf, float tmaxf,
                                            double t_min, double t_max, float& k0, float& k1, float& k2, float& k3) {
-  // the near / far plane rows picked per ray by the sign of 1/d (rows lo x y z at 0 16 32, hi x y z at
-  // 48 64 80): for 1/d >= 0, fma(lo, i, -o i) <= fma(hi, i, -o i) (the FMA rounds monotonically), so the
+  // the near / far plane rows picked per ray by the sign of 1/d (see DNode4F / DNode4C): for 1/d >= 0, fma(lo, i, -o i) <= fma(hi, i, -o i) (the FMA rounds monotonically), so the
   // pick equals the min / max of the two and each child needs only max3 / min3; a NaN (0 * inf) is
   // dropped by max3 / min3 like by the min / max form; an inverted box (lo > hi) now fails, which the
   // exact test on it never passes either (its planes cross, so hit2 misses in that axis).
   const char* nb = reinterpret_cast<const char*>(&nd);
-  const float4 nx4 = *reinterpret_cast<const float4*>(nb + r.dx);
-  const float4 fx4 = *reinterpret_cast<const float4*>((nb - r.dx) + 48);
-  const float4 ny4 = *reinterpret_cast<const float4*>(nb + (16 + r.dy));
-  const float4 fy4 = *reinterpret_cast<const float4*>((nb - r.dy) + 64);
-  const float4 nz4 = *reinterpret_cast<const float4*>(nb + (32 + r.dz));
-  const float4 fz4 = *reinterpret_cast<const float4*>((nb - r.dz) + 80);
+  float4 nx4, fx4, ny4, fy4, nz4, fz4;
+  if constexpr (N4::kRows3) {
+    const char* bx = nb + r.dx;
+    const char* by = nb + r.dy;
+    const char* bz = nb + r.dz;
+    nx4 = *reinterpret_cast<const float4*>(bx);
+    fx4 = *reinterpret_cast<const float4*>(bx + 16);
+    ny4 = *reinterpret_cast<const float4*>(by + 48);
+    fy4 = *reinterpret_cast<const float4*>(by + 64);
+    nz4 = *reinterpret_cast<const float4*>(bz + 96);
+    fz4 = *reinterpret_cast<const float4*>(bz + 112);
+  } else {
+    nx4 = *reinterpret_cast<const float4*>(nb + r.dx);
+    fx4 = *reinterpret_cast<const float4*>((nb - r.dx) + 48);
+    ny4 = *reinterpret_cast<const float4*>(nb + (16 + r.dy));
+    fy4 = *reinterpret_cast<const float4*>((nb - r.dy) + 64);
+    nz4 = *reinterpret_cast<const float4*>(nb + (32 + r.dz));
+    fz4 = *reinterpret_cast<const float4*>((nb - r.dz) + 80);
+  }
   const f32x2 ix = f2(r.ix, r.ix), iy = f2(r.iy, r.iy), iz = f2(r.iz, r.iz);
   const f32x2 nx = f2(-r.oix, -r.oix), ny = f2(-r.oiy, -r.oiy), nz = f2(-r.oiz, -r.oiz);
   float key[4];
@@ -851,7 +866,15 @@ __device__ __forceinline__ void node4_keys(const DNode4F& nd, const RayF& r, v3 
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         const double iv = comp(inv, a), oa = comp(o, a);
-        const double t0 = ((double)nd.lo[a][k] - oa) * iv, t1 = ((double)nd.hi[a][k] - oa) * iv;
+        float lo, hi;
+        if constexpr (N4::kRows3) {
+          lo = nd.row[a][0][k];
+          hi = nd.row[a][1][k];
+        } else {
+          lo = nd.lo[a][k];
+          hi = nd.hi[a][k];
+        }
+        const double t0 = ((double)lo - oa) * iv, t1 = ((double)hi - oa) * iv;
         tn = fmax(tn, fmin(t0, t1));
         tf = fmin(tf, fmax(t0, t1));
       }
@@ -995,13 +1018,13 @@ __device__ __forceinline__ void cas_u(unsigned& a, unsigned& b) {
 }
 // visit4's node part: the f32 keys of `node`'s four children, its children, and the spread mask
 // (see top_bytes) of its hit leaf children.
-template <int MODE>
-__device__ __forceinline__ unsigned node4_visit(const DScene& S, const DNode4F* lds_nodes, v3 o, v3 inv,
+template <int MODE, class N4>
+__device__ __forceinline__ unsigned node4_visit(const DScene& S, const N4* lds_nodes, v3 o, v3 inv,
                                                 const RayF& rf, double t_min, double t_best, float tmaxf, int node,
                                                 int4& ch, float& k0, float& k1, float& k2, float& k3,
                                                 unsigned& visits) {
   PH_COUNT(0);
-  const DNode4F& nd = fetch_node4<MODE>(S, lds_nodes, node);
+  const N4& nd = fetch_node4<MODE>(S, lds_nodes, node);
   ch = *reinterpret_cast<const int4*>(nd.child);
   const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
   node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
@@ -1049,7 +1072,7 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   }
 }
 template <int STRIDE, int MODE, bool EXT>
-__device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
+__device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                       v3 inv, RaySigns ns, const RayF& rf, const Recip& ra, bool ra_ok, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
                                       unsigned& top, unsigned* stk, const Rng& rk, uint64_t seed,
@@ -1069,7 +1092,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const DNode4F* lds_nodes,
 // exact leaf tests make the set of primitives that can win the reference's (see DNode4F); the closest
 // hit is the reference's up to exact ties in t.
 template <int STRIDE, int MODE, bool EXT>
-__device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
+__device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                          double t_min, double& t_best, int& face_best, unsigned* stk,
                                          const Rng& rk, uint64_t seed, unsigned& visits, unsigned& ptests
 #ifdef RT_PHASE_TIMING
@@ -1079,7 +1102,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const DNode4F* lds_nod
   PH_COUNT(23);
   const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   const RaySigns ns = ray_signs(inv);
-  const RayF rf = ray_f(S, o, inv);
+  const RayF rf = ray_f<typename Node4Sel<EXT>::T>(S, o, inv);
   const double a = len2(d);
   const Recip ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_r)
   const bool ra_ok = a >= 0x1p-300 && a <= 0x1p300;
@@ -1113,10 +1136,11 @@ struct Trav4 {
   RayF rf;
 };
 
+template <bool EXT>
 __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 d, double t_max) {
   T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
   T.ns = ray_signs(T.inv);
-  T.rf = ray_f(S, o, T.inv);
+  T.rf = ray_f<typename Node4Sel<EXT>::T>(S, o, T.inv);
   T.ra = recip(len2(d));
   T.ra_ok = T.ra.b >= 0x1p-300 && T.ra.b <= 0x1p300;
   T.t_best = t_max;
@@ -1131,7 +1155,7 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
 
 // Returns true when the traversal is complete (T.best / T.t_best / T.face hold the closest hit).
 template <int STRIDE, int MODE, bool EXT>
-__device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3 o,
+__device__ __forceinline__ bool trav4_step(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o,
                                            v3 d, double t_min, Trav4& T, unsigned* stk, const Rng& rk,
                                            uint64_t seed, unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
@@ -1140,12 +1164,12 @@ __device__ __forceinline__ bool trav4_step(const DScene& S, const DNode4F* lds_n
   return T.node < 0;
 }
 
-template <int MODE>
-__device__ __forceinline__ void stage_nodes4(const DScene& S, DNode4F* lds_nodes, DPrim* lds_prims) {
+template <int MODE, class N4>
+__device__ __forceinline__ void stage_nodes4(const DScene& S, N4* lds_nodes, DPrim* lds_prims) {
   if (MODE == kNodesGlobal) return;
   const int4* src = reinterpret_cast<const int4*>(S.nodes4);
   int4* dst = reinterpret_cast<int4*>(lds_nodes);
-  const int n16 = S.n_lds_nodes4 * (int)(sizeof(DNode4F) / 16);
+  const int n16 = S.n_lds_nodes4 * (int)(sizeof(N4) / 16);
   for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
   if (MODE == kSceneLds) {
     const int4* ps = reinterpret_cast<const int4*>(S.prims);

@@ -47,12 +47,30 @@ constexpr int32_t kLeafBox = 1 << 28;
 constexpr int32_t kLeafPrimMask = kLeafBox - 1;  // primitive index bits
 constexpr int kMaxKeyBits = 20;      // node-index bits of a traversal entry (so <= 2^20 4-wide nodes)
 constexpr int kStack4EntryBytes = 4; // one packed (entry t | node) word per 4-wide stack entry
+// Two layouts of the same node.  DNode4F (reference scenes): per axis three rows lo, hi, lo
+// (row[axis][r][child]); a ray whose 1/d is negative on the axis starts one row later (16 B), so its
+// near plane row is at 48 axis + s and its far row 16 B after it — one address add per axis and
+// visit, the reads' immediate offsets do the rest.  DNode4C (book-2 scenes, EXT kernel instances):
+// rows lo x y z, hi x y z, 112 B, so final_scene's tree still fits the wide block's LDS beside its
+// stacks; near / far rows at 16 axis + s and 16 axis + 48 - s (s = 48 when 1/d < 0), two adds per axis.
 struct alignas(16) DNode4F {
+  float row[3][3][4];
+  int32_t child[4];
+  static constexpr bool kRows3 = true;
+  static constexpr int kNegRow = 16;  // the ray's row offset on an axis where 1/d < 0
+};
+static_assert(sizeof(DNode4F) == 160, "DNode4F layout");
+struct alignas(16) DNode4C {
   float lo[3][4];  // lo[axis][child]
   float hi[3][4];
   int32_t child[4];
+  static constexpr bool kRows3 = false;
+  static constexpr int kNegRow = 48;
 };
-static_assert(sizeof(DNode4F) == 112, "DNode4F layout");
+static_assert(sizeof(DNode4C) == 112, "DNode4C layout");
+template <bool EXT> struct Node4Sel { typedef DNode4F T; };
+template <> struct Node4Sel<true> { typedef DNode4C T; };
+inline constexpr int node4_bytes(bool ext) { return ext ? (int)sizeof(DNode4C) : (int)sizeof(DNode4F); }
 
 // Where a kernel instance reads BVH nodes from (template parameter of the traversal):
 enum : int { kNodesGlobal = 0, kNodesLds = 1, kNodesMixed = 2,
@@ -124,7 +142,8 @@ struct DScene {
   int32_t n_nodes, n_prims;
   int32_t stack_depth;     // max stack entries a traversal can need
   int32_t n_lds_nodes;     // nodes [0, n_lds_nodes) are copied into LDS per block (BFS order: top levels)
-  const DNode4F* nodes4;   // the same tree collapsed to 4-wide f32 nodes (node 0 = top node)
+  const void* nodes4;      // the same tree collapsed to 4-wide f32 nodes (node 0 = top node): DNode4F, or
+                           // DNode4C when exts != null (Node4Sel<EXT>)
   int32_t n_nodes4;
   int32_t stack_depth4;    // exact worst-case stack of the 4-wide traversal
   int32_t n_lds_nodes4;    // 4-wide nodes [0, n_lds_nodes4) copied into LDS per megakernel block

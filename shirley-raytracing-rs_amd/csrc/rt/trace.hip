@@ -10,7 +10,7 @@
 //     64-unit window (ballot + popcount rank, one global atomic per 64 units);
 //   * units are enumerated tile-major (8x8 pixel tile x sample chunk x lane), so a fresh window
 //     hands a wave 64 neighbouring pixels: coherent primary rays;
-//   * 4-wide collapsed BVH with conservative f32 child boxes (112-B DNode4F) and exact f64 leaf
+//   * 4-wide collapsed BVH with conservative f32 child boxes (160-B DNode4F) and exact f64 leaf
 //     tests, nearest-first traversal, per-lane stack in LDS laid out [depth][lane] (conflict-free
 //     at any depth); for scenes that fit, the nodes, primitives and Perlin tables live in LDS too
 //     (one 1024-thread block per CU: 4 waves per SIMD at 128 VGPRs);
@@ -51,12 +51,13 @@ __global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : (EXT ?
 void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
-  DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
-  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
+  typedef typename Node4Sel<EXT>::T N4;
+  N4* lds_nodes = reinterpret_cast<N4*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(N4));
   const DPerlin* lds_perlin = (MODE == kSceneLds && P.scene.n_lds_perlin > 0)
                                   ? reinterpret_cast<const DPerlin*>(lds_prims + P.scene.n_lds_prims)
                                   : nullptr;
-  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(N4) +
                             (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) +
                                                      (size_t)P.scene.n_lds_perlin * sizeof(DPerlin)
                                                : 0);
@@ -451,9 +452,10 @@ __global__ __launch_bounds__(kHitThreads) void hit4_kernel(DScene S, const doubl
                                                            double t_min, double t_max, HitOut* __restrict__ out) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
-  DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
-  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)S.n_lds_nodes4 * sizeof(DNode4F));
-  unsigned char* stk_base = lds_raw + (size_t)S.n_lds_nodes4 * sizeof(DNode4F) +
+  typedef typename Node4Sel<EXT>::T N4;
+  N4* lds_nodes = reinterpret_cast<N4*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4));
+  unsigned char* stk_base = lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4) +
                             (MODE == kSceneLds ? (size_t)S.n_lds_prims * sizeof(DPrim) +
                                                      (size_t)S.n_lds_perlin * sizeof(DPerlin)
                                                : 0);
@@ -494,10 +496,11 @@ __global__ __launch_bounds__(kHitThreads) void hit4_kernel(DScene S, const doubl
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
-// megakernel block LDS: [n_lds_nodes4 x DNode4F][n_lds_prims x DPrim][n_lds_perlin x DPerlin]
+// megakernel block LDS: [n_lds_nodes4 x node4_bytes][n_lds_prims x DPrim][n_lds_perlin x DPerlin]
 // [stack_depth4 x threads packed entries]
-size_t trace_lds_bytes(int n_lds_nodes4, int n_lds_prims, int n_lds_perlin, int stack_depth4, int threads) {
-  return (size_t)n_lds_nodes4 * sizeof(DNode4F) + (size_t)n_lds_prims * sizeof(DPrim) +
+size_t trace_lds_bytes(int n_lds_nodes4, int node4_size, int n_lds_prims, int n_lds_perlin, int stack_depth4,
+                       int threads) {
+  return (size_t)n_lds_nodes4 * node4_size + (size_t)n_lds_prims * sizeof(DPrim) +
          (size_t)n_lds_perlin * sizeof(DPerlin) + (size_t)stack_depth4 * threads * kStack4EntryBytes;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
@@ -512,7 +515,7 @@ static int node_mode4(const DScene& S) {
 template <int THREADS, int MODE, bool EXT>
 static hipError_t occupancy_impl1(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
-  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, S.n_lds_prims, S.n_lds_perlin, S.stack_depth4, THREADS);
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(S.exts != nullptr), S.n_lds_prims, S.n_lds_perlin, S.stack_depth4, THREADS);
   hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE, EXT>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -563,7 +566,7 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
 }
 
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
-  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads);
+  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, node4_bytes(p.scene.exts != nullptr), p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads);
   if (threads == kTraceThreadsWide) {
     if (p.scene.n_lds_prims > 0)
       launch_trace1<kTraceThreadsWide, kSceneLds>(p, blocks, lds, stream);
@@ -604,7 +607,7 @@ hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, 
 template <int MODE, bool EXT>
 static hipError_t launch_hit4_1(const DScene& S, const double* rays, int n, double t_min, double t_max, HitOut* o,
                                 int blocks, hipStream_t stream) {
-  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, MODE == kSceneLds ? S.n_lds_prims : 0,
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(EXT), MODE == kSceneLds ? S.n_lds_prims : 0,
                                      MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads);
   hipError_t e = hipFuncSetAttribute((const void*)hit4_kernel<MODE, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kTraceThreadsWide, 1) void split_kernel(KParams P) 
     int slot = 0;
     v3 o = V(0.0, 0.0, 0.0), d = V(1.0, 1.0, 1.0);
     Trav4 T;
-    trav4_begin(T, S, o, d, 0.0);
+    trav4_begin<false>(T, S, o, d, 0.0);
     const Rng rk{0u, 0u, 0u, 0u, 0u};  // reference scenes only (no book-2 media draws)
     unsigned visits = 0, ptests = 0;
     int rot = wave;  // first shading wave this wave looks at (spreads the claims)
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(kTraceThreadsWide, 1) void split_kernel(KParams P) 
             const double* rp = rays + (size_t)slot * 6;
             o = V(rp[0], rp[1], rp[2]);
             d = V(rp[3], rp[4], rp[5]);
-            trav4_begin(T, S, o, d, __builtin_inf());
+            trav4_begin<false>(T, S, o, d, __builtin_inf());
             has_ray = true;
           }
           idle &= ~__ballot(take);

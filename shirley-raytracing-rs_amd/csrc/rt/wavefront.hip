@@ -143,9 +143,10 @@ template <int THREADS, bool EXT>
 __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
-  DNode4F* lds_nodes = reinterpret_cast<DNode4F*>(lds_raw);
-  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F));
-  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(DNode4F) +
+  typedef typename Node4Sel<EXT>::T N4;
+  N4* lds_nodes = reinterpret_cast<N4*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(N4));
+  unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(N4) +
                             (size_t)P.scene.n_lds_prims * sizeof(DPrim) + (size_t)P.scene.n_lds_perlin * sizeof(DPerlin);
   unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;  // [stack_depth4][THREADS] packed entries
   stage_nodes4<kSceneLds>(P.scene, lds_nodes, lds_prims);
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
   uint8_t nstate = 0;
   v3 o = V(0, 0, 0), d = V(0, 0, 0), no = V(0, 0, 0), nd = V(0, 0, 0);
   Trav4 T;
-  trav4_begin(T, S, V(0.0, 0.0, 0.0), V(1.0, 1.0, 1.0), 0.0);
+  trav4_begin<EXT>(T, S, V(0.0, 0.0, 0.0), V(1.0, 1.0, 1.0), 0.0);
   Rng rk{0u, 0u, 0u, 0u, 0u};  // side-stream key of the slot's path (read only when the scene has book-2 prims)
   unsigned visits = 0, ptests = 0, rays = 0;
   for (;;) {
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(THREADS, 1) void wf_extend4(WfParams P) {
         slot = nslot;
         o = no;
         d = nd;
-        trav4_begin(T, S, o, d, __builtin_inf());
+        trav4_begin<EXT>(T, S, o, d, __builtin_inf());
         if (S.exts) rk = Rng{st.pixel[slot], st.sample[slot], st.draw[slot], 0u, 0u};
         active = true;
         ++rays;
@@ -578,7 +579,7 @@ static int wf_mode(const DScene& S) {
 }
 
 size_t wf_extend4_lds(const DScene& S) {
-  return (size_t)S.n_lds_nodes4 * sizeof(DNode4F) + (size_t)S.n_lds_prims * sizeof(DPrim) +
+  return (size_t)S.n_lds_nodes4 * node4_bytes(S.exts != nullptr) + (size_t)S.n_lds_prims * sizeof(DPrim) +
          (size_t)S.n_lds_perlin * sizeof(DPerlin) + (size_t)S.stack_depth4 * kTraceThreadsWide * kStack4EntryBytes;
 }
 
@@ -594,6 +595,10 @@ static hipError_t prepare_one(K kernel, int threads, int lds, int* blocks_per_cu
 // The 4-wide, scene-in-LDS extend kernel for scenes where the megakernel runs wide (`S` = that scene).
 hipError_t wf_prepare4(const DScene& S, int* extend_blocks_per_cu) {
   const int lds = (int)wf_extend4_lds(S);
+  if (lds > kLdsBytes) {  // the megakernel's 768-thread block fits, this 1024-thread one does not
+    *extend_blocks_per_cu = 0;
+    return hipSuccess;
+  }
   return S.exts ? prepare_one(wf_extend4<kTraceThreadsWide, true>, kTraceThreadsWide, lds, extend_blocks_per_cu)
                 : prepare_one(wf_extend4<kTraceThreadsWide, false>, kTraceThreadsWide, lds, extend_blocks_per_cu);
 }
