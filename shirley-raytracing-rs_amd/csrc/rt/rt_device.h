@@ -814,7 +814,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f32x2 f2(float a, float b) { return f32x2{a, b}; }
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-template <class N4>
+// A missed child's key: +inf, or all ones (M1: a NaN, an inline constant, where +inf needs a v_mov
+// per visit; the LDS-node instances, +0.5 %; the L1/L2 ones measured -1 % with it).  Keys are only
+// handled as bits: either packs above every bound and entry (node4_next), and the leaf test masks
+// both out (node4_visit).
+template <bool M1, class N4>
 __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3 inv, float tminf, float tmaxf,
                                            double t_min, double t_max, float& k0, float& k1, float& k2, float& k3) {
   // the near / far plane rows picked per ray by the sign of 1/d (see DNode4F / DNode4C): for 1/d >= 0, fma(lo, i, -o i) <= fma(hi, i, -o i) (the FMA rounds monotonically), so the
@@ -856,7 +860,7 @@ __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3
     for (int e = 0; e < 2; ++e) {
       const float tn = fmaxf(fmaxf(x0[e], y0[e]), fmaxf(z0[e], tminf));
       const float tf = fminf(fminf(x1[e], y1[e]), fminf(z1[e], tmaxf));
-      key[2 * h + e] = tn <= tf ? tn : __builtin_inff();
+      key[2 * h + e] = tn <= tf ? tn : (M1 ? __uint_as_float(~0u) : __builtin_inff());
     }
   }
   if (!r.fast) {  // far origins: the same inflated boxes in f64 (exact arithmetic on a superset box)
@@ -878,7 +882,7 @@ __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3
         tn = fmax(tn, fmin(t0, t1));
         tf = fmin(tf, fmax(t0, t1));
       }
-      key[k] = tn <= tf ? __double2float_rd(tn) : __builtin_inff();
+      key[k] = tn <= tf ? __double2float_rd(tn) : (M1 ? __uint_as_float(~0u) : __builtin_inff());
     }
   }
   k0 = key[0];
@@ -921,7 +925,7 @@ __device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
   const int lo = (k & 1) ? c1 : c0, hi = (k & 1) ? c3 : c2;
   return (k & 2) ? hi : lo;
 }
-// f32 upper bound of a t, finite so that a +inf key (a miss) never passes `k <= tmaxf`.  f = (float)t
+// f32 upper bound of a t, finite so that a miss key never passes `k <= tmaxf`.  f = (float)t
 // rounds to nearest, so |t - f| <= ulp(f) / 2, and f + |f| 2^-23 >= f + ulp(f) (toward +inf for either
 // sign) is >= t after its own rounding: four instructions instead of the emulated round-up conversion
 // (~20).  The bound may be up to two f32 ulps above t: a few more subtrees kept, never one dropped.
@@ -938,7 +942,7 @@ __device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned
 template <int MODE, bool EXT>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
                                             RaySigns ns, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
-                                            int c2, int c3, double& t_best, float& tmaxf, int& best,
+                                            int c2, int c3, const int32_t* chp, double& t_best, float& tmaxf, int& best,
                                             int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
   // lm: spread mask of hit leaf children (bit 8 i + 7: child i).  A leaf's child word is
   // ~(prim | flags), so its generic / box flags (bits 29 / 28) are bits 5 / 4 of its top byte, inverted.
@@ -946,12 +950,16 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
   const unsigned gm = (nf << 2) & 0x80808080u, bm = (nf << 3) & 0x80808080u;
   unsigned sph = lm & ~gm, rect = lm & gm & ~bm, box = lm & bm;
   bool hit = false;
+  // nodes in LDS: child k's word read back from the node (one address op and one ds_read) instead of
+  // the select chain over c0..c3 (+0.3 %)
+  constexpr bool kReread = (MODE == kNodesLds || MODE == kSceneLds) && !EXT;
+  auto child = [&](int k) -> int { return kReread ? chp[k] : child_at(k, c0, c1, c2, c3); };
 #pragma unroll 1
   while (sph) {
     PH_COUNT(2);
     const int k = __builtin_ctz(sph) >> 3;
     sph &= sph - 1;
-    const int leaf = ~child_at(k, c0, c1, c2, c3);
+    const int leaf = ~child(k);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
     double t;
@@ -964,7 +972,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     PH_COUNT(4);
     const int k = __builtin_ctz(rect) >> 3;
     rect &= rect - 1;
-    const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
+    const int leaf = (~child(k)) & kLeafPrimMask;
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double b[6], te, t;
     leaf_box(pr, b);
@@ -983,7 +991,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     PH_COUNT(7);
     const int k = __builtin_ctz(box) >> 3;
     box &= box - 1;
-    const int leaf = (~child_at(k, c0, c1, c2, c3)) & kLeafPrimMask;
+    const int leaf = (~child(k)) & kLeafPrimMask;
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double te, t;
     if (EXT && pr.kind != kPrimBox) {  // an extended primitive (book 2): exact box from its DExt record
@@ -1022,29 +1030,35 @@ template <int MODE, class N4>
 __device__ __forceinline__ unsigned node4_visit(const DScene& S, const N4* lds_nodes, v3 o, v3 inv,
                                                 const RayF& rf, double t_min, double t_best, float tmaxf, int node,
                                                 int4& ch, float& k0, float& k1, float& k2, float& k3,
-                                                unsigned& visits) {
+                                                unsigned& visits, const int32_t*& chp) {
   PH_COUNT(0);
   const N4& nd = fetch_node4<MODE>(S, lds_nodes, node);
+  chp = nd.child;
   ch = *reinterpret_cast<const int4*>(nd.child);
   const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
-  node4_keys(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
+  constexpr bool kM1 = MODE == kNodesLds || MODE == kSceneLds;
+  node4_keys<kM1>(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
   RT_STAT(visits += 4);
   // hit leaf: key < inf (bits(k) + 0x80800000 keeps the sign bit exactly for bits(k) < bits(inf); keys
   // are >= 0) and a negative child word; as a spread mask
-  const unsigned h0 = (__float_as_uint(k0) + 0x80800000u) & (unsigned)ch.x;
-  const unsigned h1 = (__float_as_uint(k1) + 0x80800000u) & (unsigned)ch.y;
-  const unsigned h2 = (__float_as_uint(k2) + 0x80800000u) & (unsigned)ch.z;
-  const unsigned h3 = (__float_as_uint(k3) + 0x80800000u) & (unsigned)ch.w;
+  // (an M1 miss key ~0u: its sum keeps the top bit, so it is masked by ~bits(k) — one v_bitop3 with the
+  // child)
+  const unsigned m0 = kM1 ? ~__float_as_uint(k0) : ~0u, m1 = kM1 ? ~__float_as_uint(k1) : ~0u;
+  const unsigned m2 = kM1 ? ~__float_as_uint(k2) : ~0u, m3 = kM1 ? ~__float_as_uint(k3) : ~0u;
+  const unsigned h0 = (__float_as_uint(k0) + 0x80800000u) & m0 & (unsigned)ch.x;
+  const unsigned h1 = (__float_as_uint(k1) + 0x80800000u) & m1 & (unsigned)ch.y;
+  const unsigned h2 = (__float_as_uint(k2) + 0x80800000u) & m2 & (unsigned)ch.z;
+  const unsigned h3 = (__float_as_uint(k3) + 0x80800000u) & m3 & (unsigned)ch.w;
   return top_bytes(h0, h1, h2, h3) & 0x80808080u;
 }
-// visit4's ordering part: internal children as packed words (a miss, k = inf, packs above any
+// visit4's ordering part: internal children as packed words (a miss, k = inf or ~0u, packs above any
 // bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.
 template <int STRIDE>
 __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, float k1, float k2, float k3,
                                           float tmaxf, int& sp, unsigned& top, unsigned* stk) {
   // No select needed for leaves and empty slots: a leaf's child word is negative (top bit set) and
   // kEmptyChild is 0x7fffffff, so either word or-ed in packs above any limit (bits(tmaxf) | km <=
-  // 0x7f7fffff: tmaxf is finite and km < 2^20), as does a missed child's +inf key.
+  // 0x7f7fffff: tmaxf is finite and km < 2^20), as does a missed child's key (+inf or ~0u).
   const unsigned km = S.key_mask;
   unsigned p0 = (__float_as_uint(k0) & ~km) | (unsigned)ch.x;
   unsigned p1 = (__float_as_uint(k1) & ~km) | (unsigned)ch.y;
@@ -1079,11 +1093,12 @@ __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<E
                                       unsigned& visits, unsigned& ptests) {
   int4 ch;
   float k0, k1, k2, k3;
+  const int32_t* chp;
   const unsigned lm = node4_visit<MODE>(S, lds_nodes, o, inv, rf, t_min, t_best, tmaxf, node, ch, k0, k1, k2, k3,
-                                        visits);
+                                        visits, chp);
   if (lm) PH_COUNT(1);
   if (lm)
-    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, t_best, tmaxf, best,
+    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
                            face_best, rk, seed, ptests);
   return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
 }
