@@ -285,7 +285,9 @@ def main():
     if world == 1 and os.path.exists(tfile):  # (measured per N=1 launch; a rank's launch is smaller)
         try:
             tj = json.load(open(tfile))
-            if tj.get("workload") == f"{args.scene} {W}x{H} @ {args.spp}spp" and tj.get("bvh") == args.bvh:
+            # (the file's workload may carry the ", max_depth …" suffix of the bench's own label)
+            if (str(tj.get("workload", "")).split(",")[0] == f"{args.scene} {W}x{H} @ {args.spp}spp"
+                    and tj.get("bvh") == args.bvh):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
