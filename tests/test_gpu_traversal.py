@@ -127,13 +127,15 @@ def test_render_traversal_bbox_tree_unit_cases(gpu):
             assert _same_record(got, O.OracleScene(s).hit(ray, 0.0, MAX))
 
 
+@pytest.mark.parametrize("nodes", PLACEMENTS)
 @pytest.mark.parametrize("name", ["cornell", "box-light", "final:6:60"])
-def test_render_traversal_rect_box_and_book2_scenes(gpu, name):
+def test_render_traversal_rect_box_and_book2_scenes(gpu, name, nodes):
     """Rect / RectBox leaves (the renderer's second and third leaf loops) and book-2 extended leaves
-    (EXT kernel instance): render traversal == 2-wide traversal, record for record, and == the oracle
-    for reference primitives."""
+    (EXT kernel instance, whose 4-wide nodes use the compact 112-B layout; reference scenes the 160-B
+    lo/hi/lo rows — rt_layout.h), in every node placement: render traversal == 2-wide traversal, record
+    for record, and == the oracle for reference primitives."""
     scene = rt.SceneBuilder.builtin(name, SEED).finalize(SEED)
-    gpu.upload(scene)
+    gpu.upload(scene, nodes=nodes)
     cam = rt.scene_camera(name, 32, "square")
     eye = np.array(cam.origin)
     nodes, root = O.OracleScene(scene).tree()
