@@ -5,7 +5,8 @@ from the HIP events.  The slowest rank bounds a sharded frame, so
     predicted strong-scaling efficiency(N) = T(1) / (N * max_r T_r(N))
 (the gather, 23 MB over xGMI, is not included; it is ~0.1 % of a frame).
 
-usage: python tools/shard_balance.py [out.json] [--spp 500] [--reps 2]
+usage: python tools/shard_balance.py [out.json] [--spp 500] [--reps 2] [--worlds 1,2,4,8] [--chunk 0]
+(--chunk: a fixed sample_chunk instead of the auto choice, to compare unit lengths per world size)
 """
 import argparse
 import json
@@ -22,6 +23,7 @@ def main():
     ap.add_argument("--spp", type=int, default=500)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--worlds", default="1,2,4,8")
+    ap.add_argument("--chunk", type=int, default=0)
     a = ap.parse_args()
     import torch
     import raytracer as rt
@@ -30,14 +32,14 @@ def main():
     cam = rt.default_camera(1200, "std3x2")
     dev = rt.Device(0)
     dev.upload(scene, "sah")
-    res = {"workload": f"random 1200x800 @ {a.spp}spp, SAH, one MI355X", "worlds": {}}
+    res = {"workload": f"random 1200x800 @ {a.spp}spp, SAH, one MI355X", "chunk": a.chunk or "auto", "worlds": {}}
     t1 = None
     for world in [int(w) for w in a.worlds.split(",")]:
         n_tiles, max_tiles = rt.tile_layout(cam, world)
         buf = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
-        ms, segs = [], []
+        ms, segs, chunks = [], [], []
         for r in range(world):
-            s = rt.RenderSettings(samples=a.spp, seed=seed, tile_rank=r, tile_world=world)
+            s = rt.RenderSettings(samples=a.spp, seed=seed, tile_rank=r, tile_world=world, sample_chunk=a.chunk)
             best = None
             for _ in range(a.reps):
                 dev.render_tiles_device(cam, s, buf.data_ptr())
@@ -45,12 +47,13 @@ def main():
                 best = c.kernel_ms if best is None else min(best, c.kernel_ms)
             ms.append(best)
             segs.append(int(c.segments))
+            chunks.append(int(c.sample_chunk))
             print(f"world {world} rank {r}: {best:.2f} ms, {c.segments} segments, chunk {c.sample_chunk}", flush=True)
         if world == 1:
             t1 = ms[0]
         mx, mean = max(ms), sum(ms) / len(ms)
         res["worlds"][str(world)] = {
-            "rank_kernel_ms": [round(x, 3) for x in ms], "rank_segments": segs,
+            "rank_kernel_ms": [round(x, 3) for x in ms], "rank_segments": segs, "sample_chunk": sorted(set(chunks)),
             "max_over_mean": round(mx / mean, 4),
             "segments_max_over_mean": round(max(segs) / (sum(segs) / len(segs)), 4),
             "predicted_efficiency": round(t1 / (world * mx), 4) if t1 else None}
