@@ -30,6 +30,9 @@ hipError_t launch_split(const KParams& p, int nt, int blocks, hipStream_t stream
 #ifdef RT_PHASE_TIMING
 void phase_counters_dump();
 #endif
+#ifdef RT_TIMELINE
+void timeline_dump();
+#endif
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
                          int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
 hipError_t launch_tonemap(const double* accum, int width, int height, double inv, uint8_t* rgb8, hipStream_t stream);
@@ -1355,6 +1358,9 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
             lane / (64.0 * wave));
     phase_counters_dump();
   }
+#endif
+#ifdef RT_TIMELINE
+  timeline_dump();
 #endif
   float a = 0.f, b = 0.f;
   HIP_TRY(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));

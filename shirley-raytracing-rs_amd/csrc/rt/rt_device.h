@@ -751,6 +751,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
 static __device__ unsigned long long g_phase_ctr[64];
 // histograms of the instrumented build: node visits per traversing lane, and per wave (its slowest lane)
 static __device__ unsigned long long g_visit_hist[64], g_wave_visit_hist[64];
+
 __device__ __forceinline__ void ph_count(int i) {
   const unsigned long long act = __ballot(1);
   if ((int)__lane_id() == __builtin_ctzll(act)) {
@@ -768,6 +769,11 @@ __device__ __forceinline__ void ph_count(int i) {
 #define RT_STAT(x) x
 #else
 #define RT_STAT(x)
+#endif
+#ifdef RT_TIMELINE
+// timeline build: per-wave start, unit-pool-exhausted and exit times (s_memrealtime, 100 MHz)
+constexpr int kTimelineWaves = 1 << 16;
+static __device__ unsigned long long g_wave_t0[kTimelineWaves], g_wave_tx[kTimelineWaves], g_wave_t1[kTimelineWaves];
 #endif
 template <int MODE, class N4>
 __device__ __forceinline__ const N4& fetch_node4(const DScene& S, const N4* lds_nodes, int idx) {

@@ -19,6 +19,9 @@
 //   * per-unit partial sums go to HBM once; a reduce kernel sums chunks in order (deterministic).
 #include "rt_device.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace rt {
 
 // ------------------------------------------------------------------------------------------
@@ -88,6 +91,11 @@ void trace_kernel(KParams P) {
 
 #ifdef RT_PHASE_TIMING
   unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
+#endif
+#ifdef RT_TIMELINE
+  const unsigned wave_gid = blockIdx.x * (THREADS / kWave) + tid / kWave;
+  bool ph_exh_seen = false;
+  if (lane == 0 && wave_gid < (unsigned)kTimelineWaves) g_wave_t0[wave_gid] = __builtin_amdgcn_s_memrealtime();
 #endif
   // One iteration: (1) a ray_color segment for every lane holding a path (closest hit, record,
   // material); (2) lanes whose path ends here (sky or a light) or that hold none take the next sample
@@ -285,6 +293,12 @@ void trace_kernel(KParams P) {
 #ifdef RT_PHASE_TIMING
     ph_shade += clock64() - ph3;
 #endif
+#ifdef RT_TIMELINE
+    if (exhausted && !ph_exh_seen) {
+      ph_exh_seen = true;
+      if (lane == 0 && wave_gid < (unsigned)kTimelineWaves) g_wave_tx[wave_gid] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     // done when no lane holds a path or a unit and the pool is drained (a lane that fails to get a
     // unit while the pool is not drained — e.g. an edge tile's unit outside the image — retries)
     if (exhausted && !__any(active || has_unit)) break;
@@ -304,6 +318,9 @@ void trace_kernel(KParams P) {
       visits = ptests = 0;
     }
   }
+#ifdef RT_TIMELINE
+  if (lane == 0 && wave_gid < (unsigned)kTimelineWaves) g_wave_t1[wave_gid] = __builtin_amdgcn_s_memrealtime();
+#endif
   // wave-reduce the per-lane counters, one atomic per wave
   unsigned long long n_vis = visits, n_pt = ptests;
   for (int off = 32; off > 0; off >>= 1) {
@@ -649,6 +666,46 @@ hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, 
                      ty0, tile_rank, tile_world, width, row0, row1, packed, out);
   return hipGetLastError();
 }
+
+#ifdef RT_TIMELINE
+// timeline build: per-wave exit times of the last launch relative to the first wave's start, and each
+// wave's time from seeing the unit pool exhausted to its exit (the frame's tail)
+void timeline_dump() {
+  {
+    static unsigned long long t0[kTimelineWaves], tx[kTimelineWaves], t1[kTimelineWaves];
+    if (hipMemcpyFromSymbol(t0, HIP_SYMBOL(g_wave_t0), sizeof t0) == hipSuccess &&
+        hipMemcpyFromSymbol(tx, HIP_SYMBOL(g_wave_tx), sizeof tx) == hipSuccess &&
+        hipMemcpyFromSymbol(t1, HIP_SYMBOL(g_wave_t1), sizeof t1) == hipSuccess) {
+      std::vector<double> ends, tails, firstx;
+      unsigned long long tmin = ~0ull;
+      for (int i = 0; i < kTimelineWaves; ++i)
+        if (t1[i] && t0[i]) tmin = std::min(tmin, t0[i]);
+      for (int i = 0; i < kTimelineWaves; ++i)
+        if (t1[i] && t0[i] && t1[i] >= tmin) {
+          ends.push_back((double)(t1[i] - tmin) * 1e-2);  // 100 MHz ticks -> us
+          if (tx[i] && tx[i] <= t1[i]) {
+            tails.push_back((double)(t1[i] - tx[i]) * 1e-2);
+            firstx.push_back((double)(tx[i] - tmin) * 1e-2);
+          }
+        }
+      auto pct = [](std::vector<double> v, double q) {
+        if (v.empty()) return 0.0;
+        std::sort(v.begin(), v.end());
+        return v[std::min(v.size() - 1, (size_t)(q * (double)(v.size() - 1)))];
+      };
+      fprintf(stderr, "[phase-timeline] waves %zu; exit us p0 %.1f p50 %.1f p90 %.1f p99 %.1f p99.9 %.1f max %.1f; "
+              "pool exhausted seen at us p0 %.1f p50 %.1f; exhausted->exit us p50 %.1f p90 %.1f p99 %.1f max %.1f\n",
+              ends.size(), pct(ends, 0), pct(ends, 0.5), pct(ends, 0.9), pct(ends, 0.99), pct(ends, 0.999),
+              pct(ends, 1), pct(firstx, 0), pct(firstx, 0.5), pct(tails, 0.5), pct(tails, 0.9), pct(tails, 0.99),
+              pct(tails, 1));
+      std::fill(t0, t0 + kTimelineWaves, 0ull);
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_t0), t0, sizeof t0);
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_tx), t0, sizeof t0);
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_t1), t0, sizeof t0);
+    }
+  }
+}
+#endif
 
 #ifdef RT_PHASE_TIMING
 // instrumented build: print and clear the event counters (slot 2i: lane events, 2i + 1: wave events)
