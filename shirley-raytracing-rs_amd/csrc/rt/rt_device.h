@@ -922,7 +922,8 @@ __device__ __forceinline__ void leaf_box(const DPrim& pr, double* b) {
 }
 
 // The hit leaf children of a 4-wide node against the running closest, each exactly as
-// bbox_tree.rs:60-71 does: f64 hit2 on the object's own bounding box, then the object.  One loop per
+// bbox_tree.rs:60-71 does: f64 hit2 on the object's own bounding box and the object (for spheres
+// evaluated object first — the same conjunction of two pure functions).  One loop per
 // leaf kind — spheres (sphere.rs:28-46), rects (rect.rs:54-65), boxes (rect.rs:132-156) — each in
 // child order, so a wave runs a kind's code only while one of its lanes holds a leaf of that kind.
 // (Which of several leaves with exactly equal t wins is the one tie the reference's own tree order
@@ -967,11 +968,15 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     sph &= sph - 1;
     const int leaf = ~child(k);
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-    if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
+    // the reference's `box.hit2 && sphere.hit` (bbox_tree.rs:60-71) as `sphere.hit && box.hit2`: both are
+    // pure functions of the same (ray, t_min, t_best), so the conjunction is the same; the sphere test
+    // is the cheaper filter here (the box passes ~95 % of the trips, the sphere far fewer): +1.3 %
     double t;
     PH_COUNT(3);
     RT_STAT(++ptests);
-    if (sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) { t_best = t; best = leaf; face_best = -1; hit = true; }
+    if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) continue;
+    if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
+    t_best = t; best = leaf; face_best = -1; hit = true;
   }
 #pragma unroll 1
   while (rect) {
