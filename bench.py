@@ -167,6 +167,42 @@ def configs_block(args, dev, torch, rt):
     return out
 
 
+def sharded_config5(args, dev, comm, rank, world, torch, dist, rt, width=None, spp=None, keep=None):
+    """BASELINE config 5 as it is stated: book-2 final_scene 1920x1080 @ 2000 spp tile-sharded across the
+    job's GPUs with the RCCL gather to rank 0 (rt_render_sharded), one untimed frame (sizes the per-render
+    scratch) and one timed frame bracketed by barriers, max over ranks.  Runs after the headline's timed
+    region, so the headline number is unaffected."""
+    key, name, w0, aspect, spp0, note = OTHER_CONFIGS[3]
+    width, spp = width or w0, spp or spp0  # (smaller only in tests/test_gpu_multi.py)
+    scene = rt.SceneBuilder.builtin(name, args.seed).finalize(args.seed)
+    cam = rt.scene_camera(name, width, aspect)
+    W, H = cam.image_width, cam.image_height
+    dev.upload(scene, args.bvh)
+    settings = rt.RenderSettings(samples=spp, max_reflect=args.max_depth, seed=args.seed, tile_rank=rank,
+                                 tile_world=world)
+    accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda") if rank == 0 else None
+    sh = torch.cuda.current_stream().cuda_stream
+    ptr = accum.data_ptr() if rank == 0 else 0
+    dev.render_sharded(comm, cam, settings, ptr, sh)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dev.render_sharded(comm, cam, settings, ptr, sh)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    if keep is not None:
+        keep.append(accum)
+    return {f"{key}_sharded": {"workload": f"book-2 final_scene {W}x{H} @ {spp} spp, tile-sharded over {world} GPUs, "
+                                          "ncclGather of the packed tiles to rank 0",
+                               "value": round(W * H * spp / dt / 1e6, 3), "unit": "Msamples/s",
+                               "ms_per_frame": round(dt * 1e3, 3), "ranks": world}}
+
+
 def valu_block(segments, k_ms, W, H, args):
     """The measured ceiling of the trace kernel (VALU issue x lane utilisation), from the committed PMC
     passes (profiles/valu.json, written by tools/pmc_valu.py from profiles/<round>/pmc_valu_*.csv of one
@@ -322,6 +358,11 @@ def main():
         line["cpu_baseline"] = cpu_baseline(scene, cam, args)
     if world == 1 and not args.no_configs:  # (after the timed region; the headline scene is replaced)
         line["configs"] = configs_block(args, dev, torch, rt)
+    if comm is not None and not args.no_configs:  # config 5 at its stated scale: sharded over the job's GPUs
+        try:
+            line["configs"] = sharded_config5(args, dev, comm, rank, world, torch, dist, rt)
+        except Exception as e:  # (an extra leg: it must not cost the headline line)
+            line["configs"] = {"cfg5_final_sharded": {"error": repr(e)[:200]}}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:

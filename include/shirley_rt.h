@@ -171,7 +171,10 @@ typedef struct rt_render_params {
   int32_t tile_rank;    /* interleaved 8x8-tile sharding: this call renders tiles k with k % tile_world == tile_rank */
   int32_t tile_world;   /* 1 = whole frame */
   int32_t sample_chunk; /* samples per work unit (0 = automatic; >= samples gives in-order per-pixel sums).
-                         * The megakernel indexes work units (pixels x ceil(spp / chunk)) in 32 bits: an
+                         * Automatic usually picks chunk < samples: each chunk is summed in order, then the
+                         * chunk sums in chunk order — not render.rs:58-69's single running sum, so the
+                         * frame differs from the in-order one by reassociation only (|d| <= 1e-12 |sum|,
+                         * DESIGN.md §2).  The megakernel indexes work units (pixels x ceil(spp / chunk)) in 32 bits: an
                          * explicit chunk giving >= 2^32 units fails with RT_E_UNSUPPORTED (auto raises it). */
   int32_t engine;       /* RT_ENGINE_* (0 = automatic), optionally | RT_ENGINE_TIMING */
 } rt_render_params;

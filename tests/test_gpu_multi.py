@@ -80,3 +80,39 @@ def test_cli_gpus_flag(tmp_path):
     r = subprocess.run([cli] + common + ["-o", str(tmp_path / "b.png"), "--gpus", str(n + 1)], capture_output=True,
                        text=True)
     assert r.returncode == 1 and "rt_create" in r.stderr
+
+
+def test_bench_sharded_config5_leg(gpu):
+    """bench.py's config-5 leg (final_scene tile-sharded over the job's GPUs, rt_render_sharded + the
+    torch.distributed barrier / max-over-ranks clock) on a one-rank job, reduced size: it runs and its
+    frame equals rt_render_device's."""
+    import importlib.util
+    import os
+    import socket
+    import torch
+    import torch.distributed as dist
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    comm = gpu.comm_init_rank(rt.comm_unique_id(), 1, 0)
+    try:
+        args = bench.argparse.Namespace(seed=SEED, bvh="sah", max_depth=50)
+        keep = []
+        out = bench.sharded_config5(args, gpu, comm, 0, 1, torch, dist, rt, width=48, spp=3, keep=keep)
+        r = out["cfg5_final_sharded"]
+        assert r["value"] > 0 and r["ranks"] == 1
+        cam = rt.scene_camera("final", 48, "std16x9")
+        want = torch.zeros_like(keep[0])
+        gpu.render_device(cam, rt.RenderSettings(samples=3, max_reflect=50, seed=SEED), want.data_ptr(),
+                          torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(keep[0], want)
+    finally:
+        comm.close()
+        dist.destroy_process_group()
