@@ -5,6 +5,7 @@ bvh/bbox_tree/constructor.rs:9-212) and the C oracle, built from their sources b
 tools/sanitize/Makefile and driven by tools/sanitize/host_check.cpp: every builtin scene round-trips
 through JSON, is finalized, built and rendered; then a seeded mutation fuzzer feeds malformed and
 extreme-valued scene JSON through the same steps.  Any sanitizer report aborts the driver."""
+import fcntl
 import os
 import shutil
 import subprocess
@@ -18,7 +19,10 @@ SAN = os.path.join(REPO, "tools", "sanitize")
 @pytest.mark.skipif(shutil.which("g++") is None, reason="needs g++ with libasan/libubsan")
 @pytest.mark.parametrize("seed", ["0x5EED", "0xC0FFEE"])
 def test_host_layer_under_asan_ubsan(seed):
-    subprocess.run(["make", "-s", "-C", SAN, "build/host_check"], check=True, timeout=600)
+    os.makedirs(os.path.join(SAN, "build"), exist_ok=True)
+    with open(os.path.join(SAN, "build", ".lock"), "w") as lock:  # (xdist: one build, no relink while another runs)
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", SAN, "build/host_check"], check=True, timeout=600)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
     r = subprocess.run([os.path.join(SAN, "build", "host_check"),
