@@ -1005,7 +1005,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     // a sphere's 1 / radius (sphere.rs:48 `scale(1.0 / self.radius)`), the same IEEE quotient the device
     // would compute per hit record; p[4] is otherwise unused by spheres
     if (q.kind == kPrimSphere || q.kind == kPrimMovingSphere) q.p[4] = 1.0 / q.p[3];
-    q.material = o.material;
+    q.material = o.material | (d->materials[o.material].kind == RT_MAT_DIELECTRIC ? kPrimMatDielectric : 0);
     if (is_extended(o)) {
       if (exts.size() >= (1u << (31 - kPrimExtShift)))
         return fail(c, RT_E_UNSUPPORTED, "too many extended objects");

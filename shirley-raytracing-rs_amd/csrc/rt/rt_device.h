@@ -1149,6 +1149,90 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
   return best;
 }
 
+// traverse4 with dielectric chaining, for the megakernel on reference scenes.  A wave
+// runs its traversal loop until its slowest lane is done; a lane whose segment ends early — most often
+// a hop through the ground's glass coat (a RectBox of ir 1: one node visit) — would sit out the rest of
+// that loop and then one whole iteration of shading per hop.  Here a lane whose closest hit is a
+// dielectric and whose path goes on (depth_left > 1) scatters right away — the reference's dielectric
+// step (dielectric.rs:21-49, the same operations and draws as shade_factor with draws_coop: the uniform
+// from rng_next, drawn only without total internal reflection; attenuation 1, no emission) — and
+// starts the next segment's traversal in the same loop, on a lane that was idle.  At most CHAIN such
+// segments per call; `chained` counts them.  Returns the closest hit of the last segment, whose ray is
+// then (o, d); the caller shades it as before.
+__device__ __forceinline__ double pow5(double x);  // (below, with the materials)
+// dielectric.rs:15-19 (Schlick), inlined here (the shading's copy is out of line: `reflectance`)
+__device__ __forceinline__ double reflectance_inl(double cosine, double ref_idx) {
+  double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
+  r0 = r0 * r0;
+  return r0 + (1.0 - r0) * pow5(1.0 - cosine);
+}
+// Chaining is allowed after a traversal of at most this many node visits (RT_CHAIN_STEPS): such
+// segments end together early in the loop, so one pass of the dielectric code serves many lanes.
+#ifndef RT_CHAIN_STEPS
+#define RT_CHAIN_STEPS 1
+#endif
+template <int STRIDE, int MODE, int CHAIN>
+__device__ __forceinline__ int traverse4_chain(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3& o,
+                                               v3& d, double t_min, double& t_best, int& face_best, unsigned* stk,
+                                               Rng& rng, uint64_t seed, int& depth_left, unsigned& chained,
+                                               unsigned& visits, unsigned& ptests) {
+  v3 inv;
+  RaySigns ns;
+  RayF rf;
+  Recip ra;
+  bool ra_ok;
+  float tmaxf;
+  int best, sp, node, steps;
+  unsigned top;
+  int budget = CHAIN;
+  auto begin = [&]() {
+    inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+    ns = ray_signs(inv);
+    rf = ray_f<DNode4F>(S, o, inv);
+    const double a = len2(d);
+    ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_r)
+    ra_ok = a >= 0x1p-300 && a <= 0x1p300;
+    tmaxf = tmax_f32(t_best);
+    best = -1;
+    sp = 0;
+    top = ~0u;
+    node = S.root4;
+    steps = 0;
+  };
+  begin();
+  for (;;) {
+    if (steps < S.n_nodes4 && node >= 0) {  // (a tree traversal visits a node at most once: see traverse4)
+      node = visit4<STRIDE, MODE, false>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, ra, ra_ok, t_min, node, t_best,
+                                         tmaxf, best, face_best, sp, top, stk, rng, seed, visits, ptests);
+      ++steps;
+      continue;
+    }
+    if (budget == 0 || best < 0 || depth_left <= 1 || steps > RT_CHAIN_STEPS) break;
+    const DPrim pr = (MODE == kSceneLds) ? lds_prims[best] : S.prims[best];
+    if (!(pr.material & kPrimMatDielectric)) break;
+    // ray_color's loop body for this hit (render.rs:31-45): no emission, scatter, attenuation 1 (att
+    // unchanged, exactly), one more bounce of max_depth used
+    Hit h;
+    prim_record<false>(pr, face_best, o, d, t_best, h);
+    const DMat& m = S.mats[pr.material & kPrimMatMask];
+    const double ratio = h.front_face ? m.inv_param : m.param;  // 1.0 / ir, precomputed
+    const v3 ud = unit_fast(d);
+    const double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
+    const double sin_theta = sqrt_rn(1.0 - cos_theta * cos_theta);
+    bool refl = ratio * sin_theta > 1.0;
+    if (!refl) refl = reflectance_inl(cos_theta, ratio) > rng_next(rng, seed);  // drawn only if not TIR
+    o = h.point;
+    d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
+    --depth_left;
+    --budget;
+    ++chained;
+    t_best = __builtin_inf();
+    face_best = -1;
+    begin();
+  }
+  return best;
+}
+
 // Step-wise form for wf_extend4, where a ray's traversal state lives across loop iterations.
 struct Trav4 {
   v3 inv;
@@ -1748,11 +1832,7 @@ __device__ __forceinline__ double pow5(double x) {
 }
 
 // dielectric.rs:15-19 (Schlick); only ever compared against a uniform draw (dielectric.rs:41)
-__device__ __noinline__ double reflectance(double cosine, double ref_idx) {
-  double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
-  r0 = r0 * r0;
-  return r0 + (1.0 - r0) * pow5(1.0 - cosine);
-}
+__device__ __noinline__ double reflectance(double cosine, double ref_idx) { return reflectance_inl(cosine, ref_idx); }
 
 // skybox/mod.rs:5-25
 // skybox/mod.rs:18-25 given un = unit(d)

@@ -100,8 +100,12 @@ static_assert(sizeof(DExt) == 144, "DExt layout");
 struct alignas(16) DPrim {
   double p[6];       // sphere: cx cy cz r 1/r ; rect: d1_min d1_max d2_min d2_max offset ; box: min xyz max xyz
   int32_t kind;
-  int32_t material;
+  int32_t material;  // material index (kPrimMatMask) | kPrimMatDielectric when that material is a dielectric
 };
+// DPrim.material's flag: the megakernel chains dielectric segments inside its traversal loop
+// (traverse4_chain) and decides it from the primitive alone.
+constexpr int32_t kPrimMatDielectric = 1 << 30;
+constexpr int32_t kPrimMatMask = kPrimMatDielectric - 1;
 static_assert(sizeof(DPrim) == 64, "DPrim layout");
 
 struct alignas(16) DMat {

@@ -49,6 +49,13 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 #ifndef RT_NARROW_WAVES
 #define RT_NARROW_WAVES 4
 #endif
+// Dielectric segments a lane may chain inside one traversal call (traverse4_chain; 0 = off), reference
+// scenes only (the EXT instances keep traverse4).  Off: measured slower at every setting.
+#ifndef RT_CHAIN_MAX
+#define RT_CHAIN_MAX 0
+#endif
+constexpr int kChainMax = RT_CHAIN_MAX;
+
 template <int THREADS, int MODE, bool EXT>
 __global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : (EXT ? RT_NARROW_WAVES_EXT : RT_NARROW_WAVES))
 void trace_kernel(KParams P) {
@@ -88,6 +95,7 @@ void trace_kernel(KParams P) {
   Rng rng{0, 0, 0, 0, 0};
   unsigned long long n_seg = 0, n_samp = 0;  // wave-uniform (SGPRs): popcounts of ballots
   unsigned visits = 0, ptests = 0;           // per lane; flushed to the counters before 2^31
+  unsigned chained = 0;                      // per lane: segments chained inside traverse4_chain
 
 #ifdef RT_PHASE_TIMING
   unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
@@ -129,15 +137,19 @@ void trace_kernel(KParams P) {
       ph2 = clock64();
       ph_trav += ph2 - ph1;
 #else
-      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
-                                      ptests);
+      if constexpr (!EXT && kChainMax > 0)  // dielectric segments chained inside the traversal loop
+        prim = traverse4_chain<THREADS, MODE, kChainMax>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng,
+                                                         seed, depth_left, chained, visits, ptests);
+      else
+        prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
+                                        ptests);
 #endif
       if (prim >= 0) {
         PH_COUNT(15);
         hit = true;
         const DPrim pr = (MODE == kSceneLds) ? lds_prims[prim] : S.prims[prim];  // (LDS copy when resident)
         hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
-        mat = pr.material;
+        mat = pr.material & kPrimMatMask;
         mk = S.mats[mat].kind;
         need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
         if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
@@ -322,10 +334,11 @@ void trace_kernel(KParams P) {
   if (lane == 0 && wave_gid < (unsigned)kTimelineWaves) g_wave_t1[wave_gid] = __builtin_amdgcn_s_memrealtime();
 #endif
   // wave-reduce the per-lane counters, one atomic per wave
-  unsigned long long n_vis = visits, n_pt = ptests;
+  unsigned long long n_vis = visits, n_pt = ptests, n_ch = chained;
   for (int off = 32; off > 0; off >>= 1) {
     n_vis += __shfl_down(n_vis, off);
     n_pt += __shfl_down(n_pt, off);
+    n_ch += __shfl_down(n_ch, off);
   }
 #ifdef RT_PHASE_TIMING
   for (int off = 32; off > 0; off >>= 1) ph_lane_steps += __shfl_down(ph_lane_steps, off);
@@ -333,7 +346,7 @@ void trace_kernel(KParams P) {
 #endif
   if (lane == 0) {
     DCounters* cs = P.counters + (blockIdx.x % kCounterSlots);
-    atomicAdd(&cs->segments, n_seg);
+    atomicAdd(&cs->segments, n_seg + n_ch);
     atomicAdd(&cs->samples, n_samp);
     atomicAdd(&cs->node_visits, n_vis);
     atomicAdd(&cs->prim_tests, n_pt);
