@@ -861,7 +861,21 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   HIP_TRY(c, hipMemcpyAsync(kwork, &kp.work, sizeof(DWork), hipMemcpyHostToDevice, s));
   kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
   kp.work_const = (uint64_t)(uintptr_t)kwork;
-  HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, sizeof(unsigned long long), s));
+  {
+    // per-block unit segments (trace.hip, RT_BLOCK_SEGMENTS): one counter per megakernel block, used
+    // for units of >= 4 samples (measured, session T: headline +2 %, gen_spheres +11 %, final_scene
+    // +2.4 %, 2 ranks +2.4 %; with 1- or 2-sample units — small frames, 4 and 8 ranks — the shared
+    // queue is as fast or faster: cfg1 -17 %, the 8-rank frame -6 % with segments)
+    const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
+    const uint64_t per = (kp.work.n_units + nseg - 1) / nseg;
+    kp.work.n_segs = (engine == RT_ENGINE_MEGAKERNEL && chunk >= 4) ? (uint32_t)nseg : 0u;
+    kp.work.seg_len = (uint32_t)std::max<uint64_t>(kWave, (per + kWave - 1) / kWave * kWave);
+    const size_t bytes = std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t));
+    st = ensure(c, c->unit_counter, bytes);
+    if (st) return st;
+    kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
+    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, bytes, s));
+  }
   HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
   c->last_engine = engine;
   c->host_samples = 0;

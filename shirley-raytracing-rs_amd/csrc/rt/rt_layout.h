@@ -203,6 +203,11 @@ struct DWork {
   int32_t ty0;                   // first tile row of the window (rt_render_scanlines)
   uint64_t seed;
   uint64_t n_units;              // n_tiles_rank * n_chunks * 64
+  // megakernel with RT_BLOCK_SEGMENTS: the (tile-major) unit space cut into n_segs contiguous segments
+  // of seg_len units (a multiple of 64), one per block (XCD-major: the blocks of one XCD own adjacent
+  // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
+  // segment, then steal from the next segments that still hold units
+  uint32_t seg_len, n_segs;
 };
 
 // Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot

@@ -55,6 +55,11 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 #define RT_CHAIN_MAX 0
 #endif
 constexpr int kChainMax = RT_CHAIN_MAX;
+// Units taken from per-block segments of the unit space (stealing from other segments once the
+// block's is empty) instead of one global queue: a block's waves stay on neighbouring tiles.
+#ifndef RT_BLOCK_SEGMENTS
+#define RT_BLOCK_SEGMENTS 1
+#endif
 
 template <int THREADS, int MODE, bool EXT>
 __global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : (EXT ? RT_NARROW_WAVES_EXT : RT_NARROW_WAVES))
@@ -83,6 +88,15 @@ void trace_kernel(KParams P) {
   // wave-uniform window of unit indices
   unsigned long long w_next = 0, w_end = 0;
   bool exhausted = false;
+#if RT_BLOCK_SEGMENTS
+  // the block's segment, XCD-major: blocks are dealt round-robin to the 8 XCDs, so block b (on XCD
+  // b % 8) owns segment (b % 8) * ceil(n / 8) + b / 8 — an XCD's blocks own adjacent segments
+  uint32_t seg;
+  {
+    const uint32_t per_xcd = (W.n_segs + 7u) / 8u, s0 = (blockIdx.x % 8u) * per_xcd + blockIdx.x / 8u;
+    seg = s0 < W.n_segs ? s0 : blockIdx.x % max(W.n_segs, 1u);
+  }
+#endif
 
   // lane state
   // (kept lean: every loop-carried VGPR here competes with the 128-VGPR budget of 4 waves per SIMD)
@@ -190,12 +204,55 @@ void trace_kernel(KParams P) {
         idx = w_next + rank;
         w_next += k;
       } else {
+#if RT_BLOCK_SEGMENTS
+        unsigned long long nb = W.n_units;
+        if (W.n_segs != 0u) {
+        // the block's segment (consecutive chunks of neighbouring tiles: coherent lanes, the same
+        // subtrees in this XCD's L2), then any segment that still holds units: the 64 lanes read 64
+        // candidates' counters at once (device-coherent atomic loads) and the wave takes the first
+        // non-empty one.  A failed take means that segment is now empty for good (counters only grow),
+        // so the search ends after at most n_segs failures.
+        unsigned* ctr = reinterpret_cast<unsigned*>(P.unit_counter);
+        for (;;) {
+          unsigned off = 0;
+          if (lane == 0) off = atomicAdd(ctr + seg, (unsigned)kWave);
+          off = (unsigned)__builtin_amdgcn_readfirstlane((int)off);
+          if (off < W.seg_len && (unsigned long long)seg * W.seg_len + off < W.n_units) {
+            nb = (unsigned long long)seg * W.seg_len + off;
+            break;
+          }
+          bool found = false;
+          for (uint32_t base = 0; base < W.n_segs; base += kWave) {
+            uint32_t cand = seg + 1u + base + (uint32_t)lane;
+            if (cand >= W.n_segs) cand -= W.n_segs;
+            bool has = false;
+            if (base + (uint32_t)lane < W.n_segs) {
+              const unsigned o = __hip_atomic_load(ctr + cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              has = o < W.seg_len && (unsigned long long)cand * W.seg_len + o < W.n_units;
+            }
+            const unsigned long long m = __ballot(has);
+            if (m != 0ull) {
+              seg = (uint32_t)__builtin_amdgcn_readlane((int)cand, (int)__builtin_ctzll(m));
+              found = true;
+              break;
+            }
+          }
+          if (!found) break;
+        }
+        } else {  // one shared queue (short units: DWork.n_segs = 0)
+          nb = 0;
+          if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)kWave);
+          nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
+               (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
+        }
+#else
         unsigned long long nb = 0;
         if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)kWave);
         // the whole wave is here (the loop's control flow is uniform), so lane 0 is the first active
         // lane; readfirstlane (not a shuffle) lets the compiler keep the window in SGPRs
         nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
              (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
+#endif
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
         w_end = nb + kWave;
