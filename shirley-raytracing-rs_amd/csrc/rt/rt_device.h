@@ -1578,6 +1578,7 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
   const bool cam = kind == kDrawCam;
   const bool even = (r.draw & 1u) == 0u;
   uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
+#ifndef RT_DONOR_BLOCKS
   if (cam || ((kind == kDrawSphere || kind == kDrawDiel) && even)) {
     PH_COUNT(12);
     philox_block(seed, r.pixel, r.sample, cam ? 0u : (r.draw >> 1), a0, a1);
@@ -1586,6 +1587,58 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
     PH_COUNT(13);
     philox_block(seed, r.pixel, r.sample, cam ? 1u : (r.draw >> 1) + 1u, b0, b1);
   }
+#else
+  // RT_DONOR_BLOCKS (measured ±0 on the headline, gen_spheres -2.8 %: DESIGN.md §5; compiled out).
+  // One Philox call site for the wave: every lane evaluates one block — its block A if it needs one,
+  // else its block B.  A lane that needs both (a new sample with a lens, a sphere attempt at an even
+  // draw) gets its block B from a lane that needs none (sky, a dielectric at an odd draw, idle): the
+  // j-th such lane evaluates it for the j-th needing lane.  Needing lanes beyond the donors evaluate
+  // their block B at a second call site, which the wave skips when every lane was served.
+  const bool need_a = cam || ((kind == kDrawSphere || kind == kDrawDiel) && even);
+  const bool need_b = kind == kDrawSphere || (cam && lens);
+  const uint32_t cb = cam ? 1u : (r.draw >> 1) + 1u;
+  const bool both = need_a && need_b, idle = !need_a && !need_b;
+  const unsigned long long E = __ballot(both), D = __ballot(idle);
+  const int nE = __popcll(E), nD = __popcll(D);
+  const int rk = __popcll((both ? E : D) & lanes_below());  // rank among its kind (both / idle lanes)
+  uint32_t pix = r.pixel, smp = r.sample, c = need_a ? (cam ? 0u : (r.draw >> 1)) : cb;
+  int partner = 0;
+  bool donor = false;
+  if (E != 0ull) {  // wave-uniform
+    const int pD = __shfl(rank_owners(D), rk), pE = __shfl(rank_owners(E), rk);
+    partner = both ? pD : pE;
+    donor = idle && rk < nE;
+    const uint32_t opix = (uint32_t)__shfl((int)r.pixel, partner), osmp = (uint32_t)__shfl((int)r.sample, partner);
+    const uint32_t oc = (uint32_t)__shfl((int)cb, partner);
+    if (donor) {
+      pix = opix;
+      smp = osmp;
+      c = oc;
+    }
+  }
+  PH_COUNT(12);
+  uint64_t e0, e1;
+  philox_block(seed, pix, smp, c, e0, e1);
+  if (need_a) {
+    a0 = e0;
+    a1 = e1;
+  } else {
+    b0 = e0;
+    b1 = e1;
+  }
+  if (E != 0ull) {  // wave-uniform
+    const uint64_t g0 = (uint64_t)__shfl((long long)e0, partner), g1 = (uint64_t)__shfl((long long)e1, partner);
+    if (both) {
+      if (rk < nD) {
+        b0 = g0;
+        b1 = g1;
+      } else {
+        PH_COUNT(13);
+        philox_block(seed, r.pixel, r.sample, cb, b0, b1);
+      }
+    }
+  }
+#endif
   const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
   // the first attempts' uniforms, converted once for every kind: a sphere takes u0 u1 u2 (x y z), a
   // camera u0 u1 (jitter) and u2 u3 (disk), a dielectric u0
