@@ -813,6 +813,12 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
     if (n_pix > 0) n_chunks = std::min<long long>(n_chunks, max_partial / (n_pix * 3 * (long long)sizeof(double)));
     n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
     chunk = (int)((samples + n_chunks - 1) / n_chunks);
+    // ... but no unit longer than 16 samples while the partial buffer stays <= 8 GiB: the large-spp
+    // frames ran faster with short units (MI355X, tools/gpu_r02chunk3.sh: gen_spheres 1920x1080 @ 2000
+    // spp chunk 61 -> 16 +6.1 % (8: +6.8 %, at twice the buffer), final_scene the same frame +1.7 %,
+    // Cornell 600x600 @ 10 000 spp 54 -> 16 +0.2 %; chunks 25 / 50 on the headline frame -3 / -8 %)
+    const long long n16 = (samples + 15) / 16;
+    if (chunk > 16 && n_pix > 0 && n16 * n_pix * 3 * (long long)sizeof(double) <= (8LL << 30)) chunk = 16;
   }
   // the megakernel's per-block unit segments serve units of >= 4 samples (below): lift a shorter
   // automatic chunk to 4 while that still leaves >= 100 units per lane (measured: the 4-rank frame
