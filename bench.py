@@ -7,6 +7,13 @@ sums in HBM).  N GPUs (torchrun, one process per GPU): the frame's 8x8 tiles are
 ranks; each rank calls rt_render_sharded (C ABI), which renders its tiles into a packed buffer and
 gathers them to rank 0 with RCCL (ncclGather over xGMI, the north star's exchange step), where they
 are scattered into the [H][W][3] image: strong scaling of one frame.  Scene upload happens before the timed region; inputs are resident in HBM.
+Every step ends with the frame's sums copied into pinned host memory ("kernel start to
+gathered accumulation on host"); the device-only step time is reported beside it.
+
+Launch: `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N` (the driver's form), or
+`python bench.py --gpus N`, which starts that torchrun itself as a child process before anything touches
+the GPU.  --gpus must equal WORLD_SIZE under a launcher, and RCCL ranks may not outnumber the visible GPUs:
+both exit non-zero with a message instead of printing a mislabelled line.
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` (dominant kernel:
 the persistent trace kernel, timed with HIP events on the launch stream) and `cpu_baseline` (the f64
@@ -32,7 +39,9 @@ BYTES_PER_SEGMENT_F64 = 256
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU): under torchrun it must equal WORLD_SIZE; without a launcher "
+                         "N > 1 starts torchrun itself")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--width", type=int, default=1200)
@@ -43,6 +52,9 @@ def parse():
     ap.add_argument("--scene", default="random")
     ap.add_argument("--bvh", default="sah", choices=["reference", "sah"])
     ap.add_argument("--sample-chunk", type=int, default=0)
+    ap.add_argument("--partition", default="auto", choices=["auto", "tiles", "samples"],
+                    help="multi-GPU split of the frame (RT_PARTITION_*): interleaved tiles or sample shares")
+    ap.add_argument("--scratch-mb", type=int, default=0, help="partial-sum scratch bound per call (0: library default)")
     ap.add_argument("--nodes", default="auto", choices=["auto", "global", "half-lds", "lds"], help="BVH node placement")
     ap.add_argument("--engine", default="auto", choices=["auto", "megakernel", "wavefront", "split"])
     ap.add_argument("--timing", action="store_true", help="per-launch HIP-event timing of the wavefront kernels")
@@ -54,7 +66,45 @@ def parse():
                     help="skip the one-frame measurements of BASELINE.json's other configs (N=1 only)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N>1 (gloo only to rehearse several ranks on one GPU)")
+    ap.add_argument("--rank-env-only", action="store_true",
+                    help="(tests) every rank prints its RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* as JSON and exits "
+                         "before touching the GPU")
     return ap.parse_args()
+
+
+def rank_launch(n, argv, port=None):
+    """The torchrun command and environment that run this bench as `n` ranks (one process per GPU) when
+    `python bench.py --gpus n` is started without a launcher: (argv, env).  The parent never touches the
+    GPU; every rank reads RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* from torchrun."""
+    if port is None:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL across processes)
+    env.pop("WORLD_SIZE", None)
+    return cmd, env
+
+
+def check_world(args, environ, n_visible):
+    """How this process takes part for `--gpus args.gpus`: "single" (one process, N = 1), "launch" (spawn
+    N ranks) or "rank" (a rank of a launched job).  Raises SystemExit with a message on a mislabelled run:
+    WORLD_SIZE set and != --gpus, or more RCCL ranks than visible GPUs."""
+    n = args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}: need at least one GPU")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None and int(ws) != n:
+        raise SystemExit(f"bench.py: --gpus {n} but WORLD_SIZE={ws}: the launcher and the flag disagree")
+    if n > 1 and args.dist_backend == "nccl" and n > n_visible:
+        raise SystemExit(f"bench.py: --gpus {n} but {n_visible} visible GPU(s): one rank per GPU (RCCL refuses "
+                         "two ranks on one device); use --dist-backend gloo only to rehearse")
+    if ws is not None:
+        return "rank"
+    return "launch" if n > 1 else "single"
 
 
 def host_cpus():
@@ -226,18 +276,24 @@ def valu_block(segments, k_ms, W, H, args):
 
 def main():
     args = parse()
-    import numpy as np
     import torch
-    import torch.distributed as dist
-    import raytracer as rt
-
+    # (device_count does not initialise the GPU on this image: the launching parent stays GPU-free)
+    n_dev = torch.cuda.device_count()
+    mode = check_world(args, os.environ, n_dev)
+    if mode == "launch":
+        import subprocess
+        cmd, env = rank_launch(args.gpus, sys.argv[1:])
+        sys.exit(subprocess.run(cmd, env=env).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    n_dev = torch.cuda.device_count()
-    if world > 1 and args.dist_backend == "nccl" and world > n_dev:
-        raise SystemExit(f"bench.py: {world} ranks but {n_dev} visible GPUs: one rank per GPU (RCCL refuses "
-                         "two ranks on one device); use --dist-backend gloo only to rehearse")
+    if args.rank_env_only:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                                         "MASTER_PORT", "HSA_ENABLE_IPC_MODE_LEGACY")}), flush=True)
+        return
+    import numpy as np
+    import torch.distributed as dist
+    import raytracer as rt
     rehearsal = world > n_dev
     # --dist-backend gloo + fewer GPUs than ranks: a rehearsal of the multi-rank path on one box
     # (ranks share GPUs round-robin); the measured configuration is nccl (RCCL over xGMI)
@@ -256,7 +312,8 @@ def main():
     dev.upload(scene, args.bvh, args.nodes)
     settings = rt.RenderSettings(samples=args.spp, max_reflect=args.max_depth, seed=args.seed,
                                  sample_chunk=args.sample_chunk, tile_rank=rank, tile_world=world,
-                                 engine=args.engine, timing=args.timing)
+                                 engine=args.engine, timing=args.timing, partition=args.partition,
+                                 scratch_mb=args.scratch_mb)
     stream = torch.cuda.current_stream()
     sh = stream.cuda_stream
     accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
@@ -273,7 +330,14 @@ def main():
             packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
             from raytracer.parallel import gather_tiles
 
+    # the metric runs from kernel start to the gathered accumulation on the host, so every
+    # step ends with the [H][W][3] sums copied into pinned host memory (rank 0: after the gather)
+    host_accum = torch.empty((H, W, 3), dtype=torch.float64, pin_memory=True) if rank == 0 else None
+    ev_dev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    device_ms = []
+
     def step():
+        ev_dev[0].record(stream)
         if world == 1:
             dev.render_device(cam, settings, accum.data_ptr(), sh)
         elif comm is not None:
@@ -283,6 +347,9 @@ def main():
             gathered = gather_tiles(packed, world)
             if rank == 0:
                 dev.unpack_tiles_device(cam, world, gathered.data_ptr(), accum.data_ptr(), sh)
+        ev_dev[1].record(stream)
+        if host_accum is not None:
+            host_accum.copy_(accum, non_blocking=True)
 
     for _ in range(args.warmup):
         step()
@@ -295,11 +362,13 @@ def main():
     for _ in range(args.steps):
         step()
         c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
+        ev_dev[1].synchronize()
+        device_ms.append(ev_dev[0].elapsed_time(ev_dev[1]))
         kernel_ms.append(c.kernel_ms)
         segments.append(c.segments)
         samples.append(c.samples)
         laps.append((c.engine, c.iterations, c.slots, c.extend_ms, c.shade_ms, c.texture_ms, c.node_visits,
-                     c.prim_tests))
+                     c.prim_tests, c.passes, c.scratch_bytes, c.sample_chunk, c.n_chunks))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -312,8 +381,11 @@ def main():
 
     total_samples = W * H * args.spp * args.steps
     value = total_samples / elapsed / 1e6
-    k_ms = float(np.mean(kernel_ms))
-    seg = float(np.mean(segments))
+    # per trace-kernel launch (a frame whose partial sums exceed the scratch bound runs in several sample
+    # passes, one launch each): algorithmic bytes of a launch / its average duration
+    launches = max(1, laps[-1][8])
+    k_ms = float(np.mean(kernel_ms)) / launches
+    seg = float(np.mean(segments)) / launches
     achieved = BYTES_PER_SEGMENT * seg / (k_ms * 1e-3) / 1e9
     achieved_f64 = BYTES_PER_SEGMENT_F64 * seg / (k_ms * 1e-3) / 1e9
     traffic = None
@@ -330,7 +402,11 @@ def main():
     line = {
         "metric": "Msamples/sec (whole node) on book-1 random_scene 1200x800 @ 500spp; 1/2/4/8 GPU",
         "value": round(value, 3), "unit": "Msamples/s", "n_gpus": min(world, n_dev), "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        # ms_per_step: kernel start -> sums in pinned host memory; device_ms_per_step: the
+        # same step up to the sums in HBM (rank 0's stream, HIP events), without the device-to-host copy
+        "device_ms_per_step": round(float(np.mean(device_ms)), 3), "timed_to": "host (pinned, rank 0)",
+        "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"{args.scene} {W}x{H} @ {args.spp}spp, max_depth {args.max_depth}, seed "
                                f"{args.seed:#x}", "scene": args.scene, "width": W, "height": H, "spp": args.spp,
@@ -340,13 +416,16 @@ def main():
                    "slots": laps[-1][2],
                    "kernel_ms_split": {"extend": round(laps[-1][3], 3), "shade": round(laps[-1][4], 3),
                                        "texture": round(laps[-1][5], 3)} if args.timing else None,
-                   "segments_per_sample": round(seg / max(float(np.mean(samples)), 1.0), 4),
+                   "segments_per_sample": round(float(np.mean(segments)) / max(float(np.mean(samples)), 1.0), 4),
+                   "sample_chunk": laps[-1][10], "n_chunks": laps[-1][11], "sample_passes": laps[-1][8],
+                   "partial_scratch_bytes": laps[-1][9],
+                   "partition": args.partition if world > 1 else None,
                    # counted by the instrumented build only (RT_PHASE_TIMING): null here
-                   "node_tests_per_segment": round(laps[-1][6] / max(seg, 1), 3) if laps[-1][6] else None,
-                   "prim_tests_per_segment": round(laps[-1][7] / max(seg, 1), 3) if laps[-1][7] else None},
+                   "node_tests_per_segment": round(laps[-1][6] / max(segments[-1], 1), 3) if laps[-1][6] else None,
+                   "prim_tests_per_segment": round(laps[-1][7] / max(segments[-1], 1), 3) if laps[-1][7] else None},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3),
+                     "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3), "launches_per_step": launches,
                      "bytes_per_segment": BYTES_PER_SEGMENT, "segments_per_launch": int(seg),
                      "f64_state": {"bytes_per_segment": BYTES_PER_SEGMENT_F64, "achieved": round(achieved_f64, 2),
                                    "frac": round(achieved_f64 / HBM_PEAK_GBS, 5)},

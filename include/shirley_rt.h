@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -175,9 +175,41 @@ typedef struct rt_render_params {
                          * chunk sums in chunk order — not render.rs:58-69's single running sum, so the
                          * frame differs from the in-order one by reassociation only (|d| <= 1e-12 |sum|,
                          * DESIGN.md §2).  The megakernel indexes work units (pixels x ceil(spp / chunk)) in 32 bits: an
-                         * explicit chunk giving >= 2^32 units fails with RT_E_UNSUPPORTED (auto raises it). */
+                         * explicit chunk giving >= 2^32 units fails with RT_E_UNSUPPORTED (auto raises it).
+                         * The automatic length depends on the pixels a call renders (its tiles) and on
+                         * the device's CU count, so tile-sharded frames at different world sizes sum each
+                         * pixel's chunks differently (bits differ within the reassociation bound); pass an
+                         * explicit sample_chunk for frames that are bit-identical at every world size. */
   int32_t engine;       /* RT_ENGINE_* (0 = automatic), optionally | RT_ENGINE_TIMING */
+  /* ABI 6: the call's sample range — SURVEY.md §8(b)'s "sample range" — and its scratch bound.
+   * The call renders samples [sample_begin, sample_begin + sample_count) of every pixel (0 <= sample_begin,
+   * range within [0, samples)); sample_count == 0 means "to samples".  The output holds the sums over the
+   * range only.  The counter RNG is keyed by the global sample index, so ranges [0, k) and [k, S) render
+   * exactly the samples of one [0, S) call (the pixel sums differ by reassociation only: the per-pixel
+   * sum of two ranges is (sum of range 1) + (sum of range 2)).  Reference: render.rs:58-69's sample loop. */
+  int32_t sample_begin;
+  int32_t sample_count;
+  /* multi-GPU entry points (rt_render_sharded / rt_render_multi): how the frame is split over the ranks,
+   * RT_PARTITION_*; ignored by the single-device calls */
+  int32_t partition;
+  /* bound on the per-call partial-sum scratch in MiB (0 = default 512).  A call whose [chunks][pixels][3]
+   * f64 partial sums exceed it renders its chunks in consecutive sample passes, each reduced into the
+   * output in chunk order — the same per-pixel additions in the same order as one pass, so the frame is
+   * bit-identical for every bound. */
+  int32_t scratch_mb;
 } rt_render_params;
+
+/* ABI 6: rt_render_params.partition (multi-GPU) */
+enum {
+  RT_PARTITION_AUTO = 0,    /* the measured default per world size */
+  RT_PARTITION_TILES = 1,   /* interleaved 8x8 tiles (tile k -> rank k % world), gather of the packed tiles to
+                             * rank 0: every pixel's sum is computed on one rank, so the frame equals the
+                             * single-device frame whenever the unit length (sample_chunk) is the same */
+  RT_PARTITION_SAMPLES = 2  /* every rank renders all pixels for its share of the sample range (rank r:
+                             * [count*r/world, count*(r+1)/world) of it); the per-rank sums are exchanged by
+                             * row bands (all-to-all), summed in rank order and gathered to rank 0:
+                             * deterministic, equal to the single-device frame within reassociation */
+};
 
 typedef struct rt_scene_stats {
   int32_t n_objects;
@@ -210,6 +242,10 @@ typedef struct rt_counters {
   int32_t sample_chunk; /* ABI 4: samples per work unit the call used (auto-sized when params.sample_chunk == 0;
                          * < samples means each pixel's sum is added up per chunk, then chunk sums in order) */
   int32_t n_chunks;     /* ceil(samples / sample_chunk) */
+  /* ABI 6 */
+  int32_t passes;        /* sample passes the call used (> 1 when the partial sums exceed scratch_mb) */
+  int32_t trace_launches;/* trace-kernel launches of the call (one per pass; kernel_ms is their summed time) */
+  uint64_t scratch_bytes;/* partial-sum scratch the call used */
 } rt_counters;
 
 typedef struct rt_ctx rt_ctx;
@@ -224,6 +260,11 @@ const char* rt_last_error(const rt_ctx* ctx);
 /* ---- scene (replaces SceneBuilder::finalize, scene/mod.rs:111-137) --------------------------- */
 int rt_scene_upload(rt_ctx* ctx, const rt_scene_desc* scene, int32_t bvh_builder);
 int rt_scene_stats_get(rt_ctx* ctx, rt_scene_stats* out);
+/* ABI 6: 64-bit digest of the uploaded scene (its description and BVH builder; FNV-1a over every field),
+ * and the same digest computed on the host from a description (no device needed).  Equal scenes give
+ * equal digests; the multi-GPU calls compare them across ranks. */
+int rt_scene_digest(rt_ctx* ctx, uint64_t* out);
+int rt_scene_digest_host(const rt_scene_desc* scene, int32_t bvh_builder, uint64_t* out);
 
 /* ---- rendering (replaces main.rs:92-126 + render.rs:17-70) ----------------------------------- */
 /* Whole frame, blocking.  accum_host: [image_height][image_width][3] f64 per-pixel SUMS over the
@@ -276,8 +317,13 @@ int rt_scene_hit_ex(rt_ctx* ctx, const double* rays, int32_t n, double t_min, do
 /* ---- multi-GPU (ABI 4) -------------------------------------------------------
  * The frame's 8x8 tiles are dealt round-robin over the ranks of a communicator (tile k -> rank
  * k % world); each rank renders its tiles into a packed buffer and RCCL gathers the packed buffers to
- * rank 0 over xGMI (ncclGather), which scatters them into the [H][W][3] image.  The counter RNG is
- * keyed by the global pixel, so the frame is bit-identical for every world size.  Replaces the
+ * rank 0 over xGMI (ncclGather), which scatters them into the [H][W][3] image (RT_PARTITION_TILES), or
+ * every rank renders all pixels for a share of the samples (RT_PARTITION_SAMPLES, see above).  The
+ * counter RNG is keyed by the global pixel and sample, so a tile-sharded frame is bit-identical for every
+ * world size given an explicit sample_chunk (the automatic chunk follows the rank's pixel count).  Every
+ * ctx must hold the same scene: the calls compare the scenes' digests (rt_scene_digest) across ranks
+ * first and fail with RT_E_INVALID on a mismatch (rt_render_sharded: an 8-byte all-gather; the call
+ * synchronises the host with the stream for it).  Replaces the
  * reference's whole-machine rayon loop over scanlines (main.rs:92-126).  RCCL is loaded on first use
  * (dlopen "librccl.so.1": the copy already in the process if any); without it these calls return
  * RT_E_RCCL.
@@ -290,14 +336,17 @@ typedef struct rt_comm rt_comm;
 int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
 int rt_comm_init_rank(rt_ctx* ctx, const uint8_t id[RT_COMM_ID_BYTES], int32_t world, int32_t rank, rt_comm** out);
 int rt_comm_destroy(rt_comm* comm);
-/* One rank's share of a sharded frame, asynchronous on `stream` (NULL: the ctx's stream): render the
- * rank's tiles (params->tile_rank / tile_world are ignored: the communicator's rank and size are used),
- * gather to rank 0, and on rank 0 scatter into accum_dev ([H][W][3] f64 sums on its device; NULL on the
- * other ranks).  Every rank of the communicator must make the call (a collective). */
+/* One rank's share of a sharded frame, asynchronous on `stream` (NULL: the ctx's stream) after the scene
+ * digest check: render the rank's share (params->partition: its tiles, or all pixels for its samples;
+ * params->tile_rank / tile_world are ignored: the communicator's rank and size are used), exchange, and on
+ * rank 0 write accum_dev ([H][W][3] f64 sums on its device; NULL on the other ranks).  The sample range of
+ * params (sample_begin / sample_count) is the frame's; a sample partition splits it.  Every rank of the
+ * communicator must make the call (a collective). */
 int rt_render_sharded(rt_ctx* ctx, rt_comm* comm, const rt_camera* cam, const rt_render_params* params,
                       double* accum_dev, void* stream);
 /* The whole frame on n devices from one process, blocking; accum_host as rt_render's ([H][W][3] sums, row
- * 0 = bottom).  ctxs[0] is the root; every ctx needs the same scene uploaded.  n == 1 equals rt_render. */
+ * 0 = bottom).  ctxs[0] is the root; every ctx needs the same scene uploaded (the digests are compared
+ * first: RT_E_INVALID on a mismatch).  params->partition as rt_render_sharded's.  n == 1 equals rt_render. */
 int rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_camera* cam, const rt_render_params* params,
                     double* accum_host);
 

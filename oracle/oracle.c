@@ -1018,13 +1018,17 @@ static void cnt_add(or_counters* a, const or_counters* b) {
   a->prim_tests += b->prim_tests;
 }
 
-/* render.rs:49-70 */
+/* render.rs:49-70; samples [sample_begin, sample_begin + sample_count) of the frame's eff_samples (ABI 6
+ * sample range, 0 = to the end): render.rs:58-69's loop over that sub-range, summed in order */
 static void scanline(const or_scene* s, work_t* w, const rt_camera* cam, const rt_render_params* p, int32_t line,
                      double* buf) {
   int32_t S = eff_samples(p);
+  int32_t k0 = p->sample_begin, k1 = p->sample_count ? p->sample_begin + p->sample_count : S;
+  if (k0 < 0) k0 = 0;
+  if (k1 > S) k1 = S;
   for (int32_t idx = 0; idx < cam->image_width; ++idx) {
     v3 c = V(0.0, 0.0, 0.0);
-    for (int32_t k = 0; k < S; ++k) c = vadd(c, sample_color(s, w, cam, p, idx, line, (uint32_t)k));
+    for (int32_t k = k0; k < k1; ++k) c = vadd(c, sample_color(s, w, cam, p, idx, line, (uint32_t)k));
     buf[3 * idx + 0] = c.x;
     buf[3 * idx + 1] = c.y;
     buf[3 * idx + 2] = c.z;

@@ -152,6 +152,17 @@ struct SahBuilder {
 
   explicit SahBuilder(const std::vector<Box>& b) : boxes(b) {}
 
+  // Sort key of a centroid: a total order for std::sort (a NaN centroid — a box with NaN or opposite
+  // infinite planes — sorts as +inf; ties by object index), so the comparator is a strict weak ordering.
+  double ckey(int x, int a) const {
+    const double v = cen[x][a];
+    return v != v ? INFINITY : v;
+  }
+  bool before(int x, int y, int a) const {
+    const double kx = ckey(x, a), ky = ckey(y, a);
+    return kx < ky || (kx == ky && x < y);
+  }
+
   // Exact sweep: per axis, the objects sorted by centroid (ties by index), every split point
   // evaluated with prefix / suffix bounding boxes; items[begin, end) left in the best axis's order.
   // Returns the split position, or -1 when no split separates anything (all centroids equal).
@@ -162,9 +173,7 @@ struct SahBuilder {
     right_sa.resize(n);
     for (int a = 0; a < 3; ++a) {
       tmp.assign(items.begin() + begin, items.begin() + end);
-      std::sort(tmp.begin(), tmp.end(), [&](int x, int y) {
-        return cen[x][a] < cen[y][a] || (cen[x][a] == cen[y][a] && x < y);
-      });
+      std::sort(tmp.begin(), tmp.end(), [&](int x, int y) { return before(x, y, a); });
       Box acc = boxes[tmp[n - 1]];
       for (int i = n - 1; i >= 1; --i) {  // right_sa[i]: objects [i, n)
         if (i < n - 1) acc = surrounding(acc, boxes[tmp[i]]);
@@ -173,15 +182,13 @@ struct SahBuilder {
       acc = boxes[tmp[0]];
       for (int i = 1; i < n; ++i) {  // split before object i: left [0, i), right [i, n)
         if (i > 1) acc = surrounding(acc, boxes[tmp[i - 1]]);
-        if (cen[tmp[i - 1]][a] == cen[tmp[i]][a]) continue;  // not a separating plane
+        if (ckey(tmp[i - 1], a) == ckey(tmp[i], a)) continue;  // not a separating plane
         const double cost = surface(acc) * i + right_sa[i] * (n - i);
         if (cost < best_cost) { best_cost = cost; best_axis = a; best_i = i; }
       }
     }
     if (best_axis < 0) return -1;
-    std::sort(items.begin() + begin, items.begin() + end, [&](int x, int y) {
-      return cen[x][best_axis] < cen[y][best_axis] || (cen[x][best_axis] == cen[y][best_axis] && x < y);
-    });
+    std::sort(items.begin() + begin, items.begin() + end, [&](int x, int y) { return before(x, y, best_axis); });
     return begin + best_i;
   }
 

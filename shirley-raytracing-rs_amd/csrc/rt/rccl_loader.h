@@ -17,6 +17,8 @@ struct Rccl {
   decltype(&ncclCommDestroy) CommDestroy = nullptr;
   decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
   decltype(&ncclGather) Gather = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;  // scene-digest check of rt_render_sharded
+  decltype(&ncclAllToAll) AllToAll = nullptr;    // row-band exchange of sample-partitioned frames
   decltype(&ncclGroupStart) GroupStart = nullptr;
   decltype(&ncclGroupEnd) GroupEnd = nullptr;
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
@@ -44,6 +46,8 @@ inline Rccl load_rccl() {
   r.CommDestroy = reinterpret_cast<decltype(r.CommDestroy)>(sym("ncclCommDestroy"));
   r.CommGetAsyncError = reinterpret_cast<decltype(r.CommGetAsyncError)>(sym("ncclCommGetAsyncError"));
   r.Gather = reinterpret_cast<decltype(r.Gather)>(sym("ncclGather"));
+  r.AllGather = reinterpret_cast<decltype(r.AllGather)>(sym("ncclAllGather"));
+  r.AllToAll = reinterpret_cast<decltype(r.AllToAll)>(sym("ncclAllToAll"));
   r.GroupStart = reinterpret_cast<decltype(r.GroupStart)>(sym("ncclGroupStart"));
   r.GroupEnd = reinterpret_cast<decltype(r.GroupEnd)>(sym("ncclGroupEnd"));
   r.GetErrorString = reinterpret_cast<decltype(r.GetErrorString)>(sym("ncclGetErrorString"));

@@ -34,10 +34,12 @@ void phase_counters_dump();
 void timeline_dump();
 #endif
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
-                         int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream);
+                         int tile_world, int width, int row0, int row1, int packed, int accumulate, double* out,
+                         hipStream_t stream);
 hipError_t launch_tonemap(const double* accum, int width, int height, double inv, uint8_t* rgb8, hipStream_t stream);
 hipError_t launch_unpack(const double* gathered, int world, int max_tiles, int n_tiles_total, int tiles_x, int width,
                          int height, double* out, hipStream_t stream);
+hipError_t launch_sum_parts(const double* parts, int n_parts, long long n, double* out, hipStream_t stream);
 hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, double t_max, void* out,
                       hipStream_t stream);
 hipError_t launch_hit4(const DScene& S, bool wide, const double* rays, int n, double t_min, double t_max, void* out,
@@ -97,13 +99,17 @@ struct rt_ctx {
   hipEvent_t wf_ev[2] = {nullptr, nullptr};
   std::vector<hipEvent_t> lap_ev;    // RT_ENGINE_TIMING: one event after every launch
   bool have_timing = false;
-  int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0;
-  uint64_t last_slots = 0;
+  int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0, last_passes = 0;
+  uint64_t last_slots = 0, last_scratch = 0;
+  std::vector<hipEvent_t> pass_ev;   // before / after the trace launch of each sample pass
+  DCamera host_cam{};                // host sources of the device copies (KParams.cam_const / work_const)
+  std::vector<DWork> host_work;
+  uint64_t digest = 0;               // rt_scene_digest of the uploaded scene
   uint64_t host_samples = 0;  // samples of a frame served without a trace kernel (max_depth == 0)
   double lap_ms[3] = {0, 0, 0};
   // multi-GPU: this rank's packed tiles, the root's gathered buffer, and (root of rt_render_multi)
   // the communicators of the device set last used, kept for the next call
-  DevBuf packed, gathered;
+  DevBuf packed, gathered, parts, band, digests;
   std::vector<int> group_devices;
   std::vector<rt_comm> group_comms;
 };
@@ -130,6 +136,7 @@ int fail(rt_ctx* c, int code, const char* fmt, ...) {
 
 int ensure(rt_ctx* c, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes && b.p) return RT_OK;
+  if (c) HIP_TRY(c, hipSetDevice(c->device));  // (rt_render_multi drives several devices from one thread)
   if (b.p) {
     (void)hipFree(b.p);
     b.p = nullptr;
@@ -309,6 +316,53 @@ int validate(rt_ctx* c, const rt_scene_desc* d) {
     if (d->images[i].width < 1 || d->images[i].height < 1 || !d->images[i].rgb)
       return fail(c, RT_E_INVALID, "image %d: empty", i);
   return RT_OK;
+}
+
+// 64-bit FNV-1a digest of a scene description and its BVH builder, field by field (no struct padding
+// hashed): rt_scene_digest / the multi-GPU scene check.
+struct Fnv1a {
+  uint64_t h = 14695981039346656037ull;
+  void bytes(const void* p, size_t n) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ull;
+  }
+  template <class T>
+  void val(const T& v) { bytes(&v, sizeof v); }
+};
+uint64_t scene_digest(const rt_scene_desc* d, int32_t builder) {
+  Fnv1a f;
+  f.val(builder);
+  f.val(d->sky);
+  f.bytes(d->sky_color, sizeof d->sky_color);
+  f.val(d->n_objects);
+  for (int i = 0; i < d->n_objects; ++i) {
+    const rt_object& o = d->objects[i];
+    f.val(o.geometry); f.val(o.material); f.bytes(o.p, sizeof o.p); f.val(o.medium); f.val(o.transform);
+    f.bytes(o.q, sizeof o.q); f.val(o.density); f.val(o.rotate_y_deg); f.bytes(o.offset, sizeof o.offset);
+  }
+  f.val(d->n_materials);
+  for (int i = 0; i < d->n_materials; ++i) {
+    const rt_material& m = d->materials[i];
+    f.val(m.kind); f.val(m.texture); f.bytes(m.albedo, sizeof m.albedo); f.val(m.param);
+  }
+  f.val(d->n_textures);
+  for (int i = 0; i < d->n_textures; ++i) {
+    const rt_texture& t = d->textures[i];
+    f.val(t.kind); f.val(t.odd); f.val(t.even); f.val(t.table); f.bytes(t.color, sizeof t.color); f.val(t.scale);
+  }
+  f.val(d->n_perlin);
+  for (int i = 0; i < d->n_perlin; ++i) {
+    const rt_perlin_table& t = d->perlin[i];
+    f.bytes(t.ranfloat, sizeof t.ranfloat); f.bytes(t.perm_x, sizeof t.perm_x); f.bytes(t.perm_y, sizeof t.perm_y);
+    f.bytes(t.perm_z, sizeof t.perm_z);
+  }
+  f.val(d->n_images);
+  for (int i = 0; i < d->n_images; ++i) {
+    const rt_image& m = d->images[i];
+    f.val(m.width); f.val(m.height);
+    f.bytes(m.rgb, (size_t)m.width * m.height * 3);
+  }
+  return f.h;
 }
 
 BuiltTree build_tree(const rt_scene_desc* d, int32_t builder) {
@@ -734,7 +788,6 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
     return RT_OK;
   };
 
-  HIP_TRY(c, hipEventRecord(c->ev[0], s));
   HIP_TRY(c, wf_start(P, grid, s));
   long long iter = 1;
   // safety bound: every round advances each working slot by one segment or one regeneration
@@ -763,8 +816,7 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
     ++batch;
     if (iter > max_iters) return fail(c, RT_E_HIP, "wavefront engine did not terminate after %lld rounds", iter);
   }
-  HIP_TRY(c, hipEventRecord(c->ev[1], s));
-  c->last_iters = (int)iter;
+  c->last_iters += (int)iter;
   c->last_slots = n;
   c->last_timing = timing;
   if (timing && !lap_tag.empty()) {
@@ -776,18 +828,39 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
       HIP_TRY(c, hipEventElapsedTime(&ms, lap[i], lap[i + 1]));
       acc[lap_tag[i]] += ms;
     }
-    for (int k = 0; k < 3; ++k) c->lap_ms[k] = acc[k];
+    for (int k = 0; k < 3; ++k) c->lap_ms[k] += acc[k];  // (summed over the call's sample passes)
   }
   return RT_OK;
 }
 
-// trace + reduce for tile rows [ty0, ty1) ; out layout: packed tiles (packed=1) or rows [row0,row1)
-int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int ty0, int ty1, int row0, int row1,
-                  int packed, double* out_dev, hipStream_t s) {
+// The sample range [begin, end) of a call (rt_render_params.sample_begin / sample_count, ABI 6).
+struct SampleRange {
+  int begin = 0, end = 0;
+};
+
+int resolve_range(rt_ctx* c, const rt_render_params* p, SampleRange* r) {
+  const int S = p->samples == 0 ? 1 : p->samples;  // main.rs:75-80
+  if (p->sample_begin < 0 || p->sample_count < 0 || p->sample_begin > S ||
+      (long long)p->sample_begin + p->sample_count > S)
+    return fail(c, RT_E_INVALID, "sample range [%d, +%d) outside [0, %d)", p->sample_begin, p->sample_count, S);
+  r->begin = p->sample_begin;
+  r->end = p->sample_count ? p->sample_begin + p->sample_count : S;
+  return RT_OK;
+}
+
+constexpr long long kDefaultScratchMiB = 512;
+
+// trace + reduce of samples [R.begin, R.end) for tile rows [ty0, ty1); out layout: packed tiles
+// (packed=1) or rows [row0, row1).  The call's work units (pixel x chunk of samples) are traced in
+// sample passes of at most `scratch` bytes of partial sums each; every pass's reduce continues the
+// per-pixel chunk-order sums of the passes before it (reduce_kernel `accumulate`), so the frame is the
+// same for any number of passes.
+int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, const SampleRange& R, int ty0, int ty1,
+                  int row0, int row1, int packed, double* out_dev, hipStream_t s) {
   int st = check_render_args(c, cam, p);
   if (st) return st;
   HIP_TRY(c, hipSetDevice(c->device));
-  const int samples = p->samples == 0 ? 1 : p->samples;  // main.rs:75-80
+  const int count = R.end - R.begin;
   Layout L = layout(cam, ty0, ty1, p->tile_rank, p->tile_world);
   const long long n_pix = (long long)L.n_tiles_rank * kTilePixels;
 
@@ -799,50 +872,47 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   if (engine == RT_ENGINE_SPLIT && c->split_nt == 0) engine = RT_ENGINE_MEGAKERNEL;  // scene not eligible
 
   // samples per unit: ~256 units per resident lane, so that a wave's last units (its lanes finish at
-  // different times) cost little.  Short units only add partial-sum traffic (24 B written + read per
-  // unit), so the partial buffer is the only bound: <= 2 GiB.  (MI355X: headline frame chunk 23 -> 8
-  // +0.5 %, final_scene 19 -> 7 +5 %, gen_spheres @ 16 spp 3 -> 1 +24 %.)  The wavefront engine keeps
-  // its own unit length (its slots regenerate every iteration anyway).
+  // different times) cost little, and no unit longer than 16 samples (MI355X: headline frame chunk
+  // 23 -> 8 +0.5 %, final_scene 19 -> 7 +5 %, gen_spheres @ 16 spp 3 -> 1 +24 %; the 1920x1080 @ 2000
+  // spp frames 61 -> 16 +1.5-6 %, tools/gpu_r02chunk3.sh; chunks 25 / 50 on the headline frame -3 / -8 %).
+  // Short units cost only partial-sum traffic (24 B written + read per unit); the scratch they need is
+  // bounded by the sample passes below, not by the unit length.  The wavefront engine keeps its own
+  // unit length (its slots regenerate every iteration anyway).
+  const long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
+  const int work = std::max(1, count);
   int chunk = p->sample_chunk;
   if (chunk == 0 && engine == RT_ENGINE_WAVEFRONT) chunk = kWfDefaultChunk;
   if (chunk == 0) {
-    const long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
     const long long want_units = 256 * lanes;
     long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
-    const long long max_partial = 2LL << 30;  // bytes of [n_chunks][n_pix][3] f64
-    if (n_pix > 0) n_chunks = std::min<long long>(n_chunks, max_partial / (n_pix * 3 * (long long)sizeof(double)));
-    n_chunks = std::max(1LL, std::min<long long>(n_chunks, samples));
-    chunk = (int)((samples + n_chunks - 1) / n_chunks);
-    // ... but no unit longer than 16 samples while the partial buffer stays <= 8 GiB: the large-spp
-    // frames ran faster with short units (MI355X, tools/gpu_r02chunk3.sh: gen_spheres 1920x1080 @ 2000
-    // spp chunk 61 -> 16 +6.1 % (8: +6.8 %, at twice the buffer), final_scene the same frame +1.7 %,
-    // Cornell 600x600 @ 10 000 spp 54 -> 16 +0.2 %; chunks 25 / 50 on the headline frame -3 / -8 %)
-    const long long n16 = (samples + 15) / 16;
-    if (chunk > 16 && n_pix > 0 && n16 * n_pix * 3 * (long long)sizeof(double) <= (8LL << 30)) chunk = 16;
+    n_chunks = std::max(1LL, std::min<long long>(n_chunks, work));
+    chunk = std::min(16, (int)((work + n_chunks - 1) / n_chunks));
+    // the megakernel's per-block unit segments serve units of >= 4 samples (below): lift a shorter
+    // automatic chunk to 4 while that still leaves >= 100 units per lane (measured: the 4-rank frame
+    // 47.6 -> 47.1 ms; with fewer units per lane — 8 ranks, 57 — the longer units' end costs more than
+    // the segments gain, 24.5 -> 24.9 ms)
+    if (engine == RT_ENGINE_MEGAKERNEL && chunk < 4 && work >= 4 && n_pix > 0 && n_pix * ((work + 3) / 4) >= 100 * lanes)
+      chunk = 4;
   }
-  // the megakernel's per-block unit segments serve units of >= 4 samples (below): lift a shorter
-  // automatic chunk to 4 while that still leaves >= 100 units per lane (measured: the 4-rank frame
-  // 47.6 -> 47.1 ms; with fewer units per lane — 8 ranks, 57 — the longer units' end costs more than
-  // the segments gain, 24.5 -> 24.9 ms)
-  if (p->sample_chunk == 0 && engine == RT_ENGINE_MEGAKERNEL && chunk < 4 && samples >= 4 && n_pix > 0) {
-    const long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
-    const long long units4 = n_pix * ((samples + 3) / 4);
-    if (units4 >= 100 * lanes && units4 * 3 * (long long)sizeof(double) <= (2LL << 30)) chunk = 4;
-  }
-  chunk = std::max(1, std::min(chunk, samples));
-  if (engine == RT_ENGINE_MEGAKERNEL || engine == RT_ENGINE_SPLIT) {
-    // the megakernel indexes units and partial slots (n_pix * n_chunks) in 32 bits
-    const long long max_chunks = n_pix > 0 ? 0xffffffffLL / n_pix : samples;
-    if (max_chunks < 1) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
-    if ((samples + chunk - 1) / chunk > max_chunks) {
-      if (p->sample_chunk != 0)
-        return fail(c, RT_E_UNSUPPORTED, "sample_chunk %d: more than 2^32 work units", p->sample_chunk);
-      chunk = (int)((samples + max_chunks - 1) / max_chunks);
-    }
-  }
-  const int n_chunks = (samples + chunk - 1) / chunk;
+  chunk = std::max(1, std::min(chunk, work));
+  const int n_chunks = (work + chunk - 1) / chunk;
 
-  st = ensure(c, c->partial, (size_t)std::max<long long>(1, n_pix * n_chunks * 3) * sizeof(double));
+  // sample passes: at most `budget` bytes of [chunks][pixels][3] f64 partial sums per pass
+  long long budget = (long long)(p->scratch_mb > 0 ? p->scratch_mb : kDefaultScratchMiB) << 20;
+  if (p->scratch_mb == 0)
+    if (const char* e = getenv("SHIRLEY_SCRATCH_MB")) budget = std::max(1LL, atoll(e)) << 20;  // tuning
+  const long long chunk_bytes = std::max<long long>(1, n_pix * 3 * (long long)sizeof(double));
+  int per_pass = (int)std::max(1LL, std::min<long long>(n_chunks, budget / chunk_bytes));
+  if (engine == RT_ENGINE_MEGAKERNEL || engine == RT_ENGINE_SPLIT) {
+    // the megakernel indexes a pass's units and partial slots (n_pix * chunks) in 32 bits
+    const long long max_chunks = n_pix > 0 ? 0xffffffffLL / n_pix : n_chunks;
+    if (max_chunks < 1) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
+    per_pass = (int)std::min<long long>(per_pass, max_chunks);
+  }
+  const int passes = (n_chunks + per_pass - 1) / per_pass;
+  per_pass = (n_chunks + passes - 1) / passes;  // even passes
+  const size_t partial_bytes = (size_t)std::max<long long>(1, n_pix * per_pass * 3) * sizeof(double);
+  st = ensure(c, c->partial, partial_bytes);
   if (st) return st;
 
   KParams kp{};
@@ -856,80 +926,104 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, in
   kp.work.tile_rank = p->tile_rank;
   kp.work.tile_world = p->tile_world;
   kp.work.n_tiles_rank = L.n_tiles_rank;
-  kp.work.samples = samples;
   kp.work.chunk = chunk;
-  kp.work.n_chunks = n_chunks;
   kp.work.max_depth = p->max_depth;
   kp.work.seed = p->seed;
-  kp.work.n_units = (uint64_t)n_pix * (uint64_t)n_chunks;
-  kp.work.div_unit_tile = make_udiv((uint32_t)n_chunks * (uint32_t)kTilePixels);
   kp.work.div_tiles_x = make_udiv((uint32_t)L.tiles_x);
   kp.partial = static_cast<double*>(c->partial.p);
-  kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
   kp.counters = static_cast<DCounters*>(c->counters.p);
 
-  // device copies of the camera and the work descriptor (KParams.cam_const / work_const)
-  st = ensure(c, c->kcam, 2 * sizeof(DCamera) + sizeof(DWork));
+  // device copies of the camera and of each pass's work descriptor (KParams.cam_const / work_const);
+  // their host sources stay alive in the ctx until the next call
+  st = ensure(c, c->kcam, 2 * sizeof(DCamera) + (size_t)passes * sizeof(DWork));
   if (st) return st;
-  HIP_TRY(c, hipMemcpyAsync(c->kcam.p, &kp.cam, sizeof(DCamera), hipMemcpyHostToDevice, s));
-  void* kwork = static_cast<char*>(c->kcam.p) + 2 * sizeof(DCamera);  // (16-B aligned)
-  HIP_TRY(c, hipMemcpyAsync(kwork, &kp.work, sizeof(DWork), hipMemcpyHostToDevice, s));
+  c->host_cam = kp.cam;
+  c->host_work.assign(passes, DWork{});
+  HIP_TRY(c, hipMemcpyAsync(c->kcam.p, &c->host_cam, sizeof(DCamera), hipMemcpyHostToDevice, s));
   kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
-  kp.work_const = (uint64_t)(uintptr_t)kwork;
+
+  const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
   {
-    // per-block unit segments (trace.hip, RT_BLOCK_SEGMENTS): one counter per megakernel block, used
-    // for units of >= 4 samples (measured, session T: headline +2 %, gen_spheres +11 %, final_scene
-    // +2.4 %, 2 ranks +2.4 %; with 1- or 2-sample units — small frames, 4 and 8 ranks — the shared
-    // queue is as fast or faster: cfg1 -17 %, the 8-rank frame -6 % with segments)
-    const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
-    const uint64_t per = (kp.work.n_units + nseg - 1) / nseg;
-    kp.work.n_segs = (engine == RT_ENGINE_MEGAKERNEL && chunk >= 4) ? (uint32_t)nseg : 0u;
-    kp.work.seg_len = (uint32_t)std::max<uint64_t>(kWave, (per + kWave - 1) / kWave * kWave);
     const size_t bytes = std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t));
     st = ensure(c, c->unit_counter, bytes);
     if (st) return st;
     kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
-    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, bytes, s));
+  }
+  if ((int)c->pass_ev.size() < 2 * passes) {
+    const size_t have = c->pass_ev.size();
+    c->pass_ev.resize(2 * passes, nullptr);
+    for (size_t i = have; i < c->pass_ev.size(); ++i) HIP_TRY(c, hipEventCreate(&c->pass_ev[i]));
   }
   HIP_TRY(c, hipMemsetAsync(c->counters.p, 0, kCounterSlots * sizeof(DCounters), s));
   c->last_engine = engine;
   c->host_samples = 0;
   c->last_chunk = chunk;
   c->last_n_chunks = n_chunks;
+  c->last_passes = 0;
+  c->last_scratch = partial_bytes;
   c->last_iters = 0;
   c->last_slots = 0;
   c->last_timing = 0;
-  if (engine == RT_ENGINE_WAVEFRONT) {
-    st = run_wavefront(c, kp, timing, s);
-    if (st) return st;
-  } else {
-    const int blocks = std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
-    HIP_TRY(c, hipEventRecord(c->ev[0], s));
-    if (n_pix > 0 && p->max_depth == 0) {
-      // ray_color's loop never runs (render.rs:30): every sample is black.  The megakernel's exit
-      // test assumes a held unit always has an active path (true for max_depth > 0), so this case
-      // is served here: all-zero partials, reduced like any frame; the samples counter counts the
-      // window's in-image pixels of this rank's tiles, as the kernel would.
-      HIP_TRY(c, hipMemsetAsync(kp.partial, 0, (size_t)n_pix * n_chunks * 3 * sizeof(double), s));
-      uint64_t inside = 0;
-      for (long long lt = 0; lt < L.n_tiles_rank; ++lt) {
-        const long long gt = lt * p->tile_world + p->tile_rank;
-        const int tx = (int)(gt % L.tiles_x), ty = ty0 + (int)(gt / L.tiles_x);
-        const int w = std::min(kTile, cam->image_width - tx * kTile), h = std::min(kTile, cam->image_height - ty * kTile);
-        if (w > 0 && h > 0) inside += (uint64_t)w * (uint64_t)h;
-      }
-      c->host_samples = inside * (uint64_t)samples;
-    } else if (n_pix > 0 && engine == RT_ENGINE_SPLIT) {
+  for (double& x : c->lap_ms) x = 0.0;
+  HIP_TRY(c, hipEventRecord(c->ev[0], s));
+  const bool trace = n_pix > 0 && count > 0 && p->max_depth > 0;
+  if (!trace) {
+    // nothing to trace: ray_color's loop never runs with max_depth == 0 (render.rs:30: every sample is
+    // black), or the range is empty.  The window is written by a reduce over no chunks (zeros); the
+    // samples counter counts the window's in-image pixels of this rank's tiles, as the kernel would.
+    uint64_t inside = 0;
+    for (long long lt = 0; lt < L.n_tiles_rank; ++lt) {
+      const long long gt = lt * p->tile_world + p->tile_rank;
+      const int tx = (int)(gt % L.tiles_x), ty = ty0 + (int)(gt / L.tiles_x);
+      const int w = std::min(kTile, cam->image_width - tx * kTile), h = std::min(kTile, cam->image_height - ty * kTile);
+      if (w > 0 && h > 0) inside += (uint64_t)w * (uint64_t)h;
+    }
+    c->host_samples = inside * (uint64_t)count;
+    HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    if (n_pix > 0)
+      HIP_TRY(c, launch_reduce(kp.partial, 0, L.n_tiles_rank, L.tiles_x, ty0, p->tile_rank, p->tile_world,
+                               cam->image_width, row0, row1, packed, 0, out_dev, s));
+    HIP_TRY(c, hipEventRecord(c->ev[2], s));
+    c->have_timing = true;
+    return RT_OK;
+  }
+  for (int k = 0; k < passes; ++k) {
+    const int c0 = k * per_pass, c1 = std::min(n_chunks, c0 + per_pass);
+    DWork& w = kp.work;
+    w.sample_base = R.begin + c0 * chunk;
+    w.samples = (int)std::min<long long>(R.end, (long long)R.begin + (long long)c1 * chunk);
+    w.n_chunks = c1 - c0;
+    w.n_units = (uint64_t)n_pix * (uint64_t)w.n_chunks;
+    w.div_unit_tile = make_udiv((uint32_t)w.n_chunks * (uint32_t)kTilePixels);
+    // per-block unit segments (trace.hip, RT_BLOCK_SEGMENTS): one counter per megakernel block, used
+    // for units of >= 4 samples (measured, session T: headline +2 %, gen_spheres +11 %, final_scene
+    // +2.4 %, 2 ranks +2.4 %; with 1- or 2-sample units — small frames, 4 and 8 ranks — the shared
+    // queue is as fast or faster: cfg1 -17 %, the 8-rank frame -6 % with segments)
+    const uint64_t per = (w.n_units + nseg - 1) / nseg;
+    w.n_segs = (engine == RT_ENGINE_MEGAKERNEL && chunk >= 4) ? (uint32_t)nseg : 0u;
+    w.seg_len = (uint32_t)std::max<uint64_t>(kWave, (per + kWave - 1) / kWave * kWave);
+    // the device copy is taken after every field is set (the kernel may read any of them)
+    c->host_work[k] = w;
+    void* kwork = static_cast<char*>(c->kcam.p) + 2 * sizeof(DCamera) + (size_t)k * sizeof(DWork);  // (16-B aligned)
+    HIP_TRY(c, hipMemcpyAsync(kwork, &c->host_work[k], sizeof(DWork), hipMemcpyHostToDevice, s));
+    kp.work_const = (uint64_t)(uintptr_t)kwork;
+    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t)), s));
+    HIP_TRY(c, hipEventRecord(c->pass_ev[2 * k], s));
+    if (engine == RT_ENGINE_WAVEFRONT) {
+      st = run_wavefront(c, kp, timing, s);
+      if (st) return st;
+    } else if (engine == RT_ENGINE_SPLIT) {
       kp.split_refill = c->split_refill;
       HIP_TRY(c, launch_split(kp, c->split_nt, c->cu_count, s));
-    } else if (n_pix > 0) {
-      HIP_TRY(c, launch_trace(kp, blocks, c->mk_threads, s));
+    } else {
+      HIP_TRY(c, launch_trace(kp, (int)nseg, c->mk_threads, s));
     }
-    HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    HIP_TRY(c, hipEventRecord(c->pass_ev[2 * k + 1], s));
+    if (k == passes - 1) HIP_TRY(c, hipEventRecord(c->ev[1], s));
+    HIP_TRY(c, launch_reduce(kp.partial, w.n_chunks, L.n_tiles_rank, L.tiles_x, ty0, p->tile_rank, p->tile_world,
+                             cam->image_width, row0, row1, packed, k > 0 ? 1 : 0, out_dev, s));
+    c->last_passes = k + 1;
   }
-  if (n_pix > 0)
-    HIP_TRY(c, launch_reduce(kp.partial, n_chunks, L.n_tiles_rank, L.tiles_x, ty0, p->tile_rank, p->tile_world,
-                             cam->image_width, row0, row1, packed, out_dev, s));
   HIP_TRY(c, hipEventRecord(c->ev[2], s));
   c->have_timing = true;
   return RT_OK;
@@ -983,7 +1077,8 @@ int rt_destroy(rt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->exts, &c->partial, &c->kcam,
-                    &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters, &c->packed, &c->gathered})
+                    &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters, &c->packed, &c->gathered,
+                    &c->parts, &c->band, &c->digests})
     release(*b);
   for (rt_comm& m : c->group_comms)
     if (m.comm) (void)rccl().CommDestroy(m.comm);
@@ -1241,7 +1336,23 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->stats.device_bytes = (int64_t)(nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim) +
                                     mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex) +
                                     perl.size() * sizeof(DPerlin) + imgs.size() * sizeof(DImage) + texels.size());
+  c->digest = scene_digest(d, builder);
   c->have_scene = true;
+  return RT_OK;
+}
+
+int rt_scene_digest(rt_ctx* c, uint64_t* out) {
+  if (!c || !out) return RT_E_INVALID;
+  if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded");
+  *out = c->digest;
+  return RT_OK;
+}
+
+int rt_scene_digest_host(const rt_scene_desc* d, int32_t builder, uint64_t* out) {
+  if (!d || !out) return RT_E_INVALID;
+  if (validate(nullptr, d)) return RT_E_INVALID;
+  const int32_t placement_mask = RT_BVH_NODES_GLOBAL | RT_BVH_NODES_HALF_LDS | RT_BVH_NODES_LDS;
+  *out = scene_digest(d, builder & ~placement_mask);
   return RT_OK;
 }
 
@@ -1266,7 +1377,9 @@ int rt_render_device(rt_ctx* c, const rt_camera* cam, const rt_render_params* p,
   hipStream_t s;
   resolve_stream(c, stream, &s);
   int tiles_y = cam ? (cam->image_height + kTile - 1) / kTile : 0;
-  return render_window(c, cam, p, 0, tiles_y, 0, cam ? cam->image_height : 0, 0, accum_dev, s);
+  SampleRange R;
+  if (p && resolve_range(c, p, &R)) return RT_E_INVALID;
+  return render_window(c, cam, p, R, 0, tiles_y, 0, cam ? cam->image_height : 0, 0, accum_dev, s);
 }
 
 int rt_render_tiles_device(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, double* packed_dev,
@@ -1275,7 +1388,9 @@ int rt_render_tiles_device(rt_ctx* c, const rt_camera* cam, const rt_render_para
   hipStream_t s;
   resolve_stream(c, stream, &s);
   int tiles_y = cam ? (cam->image_height + kTile - 1) / kTile : 0;
-  return render_window(c, cam, p, 0, tiles_y, 0, cam ? cam->image_height : 0, 1, packed_dev, s);
+  SampleRange R;
+  if (p && resolve_range(c, p, &R)) return RT_E_INVALID;
+  return render_window(c, cam, p, R, 0, tiles_y, 0, cam ? cam->image_height : 0, 1, packed_dev, s);
 }
 
 int rt_unpack_tiles_device(rt_ctx* c, const rt_camera* cam, int32_t world, const double* gathered_dev,
@@ -1310,7 +1425,9 @@ int rt_render_scanlines(rt_ctx* c, const rt_camera* cam, const rt_render_params*
   int st = ensure(c, c->accum, bytes);
   if (st) return st;
   int ty0 = line_begin / kTile, ty1 = (line_end + kTile - 1) / kTile;
-  st = render_window(c, cam, p, ty0, ty1, line_begin, line_end, 0, static_cast<double*>(c->accum.p), c->stream);
+  SampleRange R;
+  if (p && resolve_range(c, p, &R)) return RT_E_INVALID;
+  st = render_window(c, cam, p, R, ty0, ty1, line_begin, line_end, 0, static_cast<double*>(c->accum.p), c->stream);
   if (st) return st;
   HIP_TRY(c, hipMemcpyAsync(rows_host, c->accum.p, bytes, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1391,11 +1508,21 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
 #ifdef RT_TIMELINE
   timeline_dump();
 #endif
-  float a = 0.f, b = 0.f;
-  HIP_TRY(c, hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-  HIP_TRY(c, hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-  out->kernel_ms = a;
-  out->reduce_ms = b;
+  // kernel_ms: the trace launches of the call (one per sample pass); reduce_ms: the rest of the call's
+  // device time (the reduces)
+  float all = 0.f;
+  HIP_TRY(c, hipEventElapsedTime(&all, c->ev[0], c->ev[2]));
+  double trace = 0.0;
+  for (int k = 0; k < c->last_passes; ++k) {
+    float t = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&t, c->pass_ev[2 * k], c->pass_ev[2 * k + 1]));
+    trace += t;
+  }
+  out->kernel_ms = trace;
+  out->reduce_ms = std::max(0.0, (double)all - trace);
+  out->passes = c->last_passes;
+  out->trace_launches = c->last_passes;
+  out->scratch_bytes = c->last_scratch;
   out->engine = c->last_engine;
   out->sample_chunk = c->last_chunk;
   out->n_chunks = c->last_n_chunks;
@@ -1472,32 +1599,109 @@ int need_rccl(rt_ctx* c) {
   return RT_OK;
 }
 
-// One rank's part before the gather: its tiles rendered into c->packed (rank 0 also sizes the
-// gathered buffer).  *count = doubles per rank in the gather.
-int shard_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int world, int rank, hipStream_t s,
-                 size_t* count) {
+// Partition of a multi-GPU frame (rt_render_params.partition): RT_PARTITION_AUTO picks the measured
+// default; SHIRLEY_PARTITION=tiles|samples overrides it (tuning).
+int frame_partition(rt_ctx* c, const rt_render_params* p, int world, int* out) {
+  int part = p->partition;
+  if (part < RT_PARTITION_AUTO || part > RT_PARTITION_SAMPLES) return fail(c, RT_E_INVALID, "bad partition %d", part);
+  if (part == RT_PARTITION_AUTO) {
+    part = RT_PARTITION_TILES;
+    if (const char* e = getenv("SHIRLEY_PARTITION")) part = !strcmp(e, "samples") ? RT_PARTITION_SAMPLES : RT_PARTITION_TILES;
+  }
+  (void)world;
+  *out = part;
+  return RT_OK;
+}
+
+// Row bands of a sample-partitioned frame: rank b owns rows [b * band_rows, (b + 1) * band_rows).
+int band_rows(const rt_camera* cam, int world) { return (cam->image_height + world - 1) / world; }
+
+// One rank's share before the exchange.
+//   tiles: its tiles rendered into c->packed ([max_tiles][64][3]); *count = doubles per rank of the gather
+//     (rank 0 also sizes the gathered buffer).
+//   samples: all pixels for its part of the frame's sample range, rendered into c->packed as
+//     [world * band_rows][W][3] (rows >= H zero); *count = doubles of one row band.
+int shard_render(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int part, int world, int rank,
+                 hipStream_t s, size_t* count) {
   int st = check_render_args(c, cam, p);
   if (st) return st;
+  HIP_TRY(c, hipSetDevice(c->device));
+  SampleRange R;
+  if ((st = resolve_range(c, p, &R))) return st;
+  rt_render_params q = *p;
+  q.tile_rank = 0;
+  q.tile_world = 1;
+  const int tiles_y = (cam->image_height + kTile - 1) / kTile;
+  if (part == RT_PARTITION_SAMPLES) {
+    const int rows = band_rows(cam, world);
+    *count = (size_t)rows * cam->image_width * 3;
+    const size_t total = *count * world;
+    if ((st = ensure(c, c->packed, total * sizeof(double)))) return st;
+    if ((st = ensure(c, c->parts, total * sizeof(double)))) return st;
+    if ((st = ensure(c, c->band, *count * sizeof(double)))) return st;
+    if (rank == 0 && (st = ensure(c, c->gathered, total * sizeof(double)))) return st;
+    const size_t image = (size_t)cam->image_height * cam->image_width * 3;
+    double* local = static_cast<double*>(c->packed.p);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (total > image) HIP_TRY(c, hipMemsetAsync(local + image, 0, (total - image) * sizeof(double), s));
+    const long long n = R.end - R.begin;
+    SampleRange mine;
+    mine.begin = R.begin + (int)(n * rank / world);
+    mine.end = R.begin + (int)(n * (rank + 1) / world);
+    return render_window(c, cam, &q, mine, 0, tiles_y, 0, cam->image_height, 0, local, s);
+  }
   int32_t n_total = 0, max_tiles = 0;
   if (rt_tile_layout(cam, world, &n_total, &max_tiles)) return fail(c, RT_E_INVALID, "bad tile layout");
   *count = (size_t)max_tiles * kTilePixels * 3;
   if ((st = ensure(c, c->packed, std::max<size_t>(*count, 1) * sizeof(double)))) return st;
   if (rank == 0 && (st = ensure(c, c->gathered, std::max<size_t>(*count * world, 1) * sizeof(double)))) return st;
-  rt_render_params q = *p;
   q.tile_rank = rank;
   q.tile_world = world;
-  const int tiles_y = (cam->image_height + kTile - 1) / kTile;
-  return render_window(c, cam, &q, 0, tiles_y, 0, cam->image_height, 1, static_cast<double*>(c->packed.p), s);
+  return render_window(c, cam, &q, R, 0, tiles_y, 0, cam->image_height, 1, static_cast<double*>(c->packed.p), s);
 }
 
-// Root: gathered [world][max_tiles][64][3] -> accum_dev [H][W][3].
-int shard_unpack(rt_ctx* c, const rt_camera* cam, int world, double* accum_dev, hipStream_t s) {
+// samples partition, after the all-to-all (c->parts = [world][band] partial bands of this rank's rows):
+// the rank-order sum of its band
+int shard_band_sum(rt_ctx* c, int world, size_t count, hipStream_t s) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, launch_sum_parts(static_cast<const double*>(c->parts.p), world, (long long)count,
+                              static_cast<double*>(c->band.p), s));
+  return RT_OK;
+}
+
+// Root: the gathered buffer -> accum_dev [H][W][3] (tiles: scatter the packed tiles; samples: the
+// gathered row bands are the image's rows in order, padding rows dropped).
+int shard_unpack(rt_ctx* c, const rt_camera* cam, int part, int world, double* accum_dev, hipStream_t s) {
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (part == RT_PARTITION_SAMPLES) {
+    const size_t bytes = (size_t)cam->image_height * cam->image_width * 3 * sizeof(double);
+    HIP_TRY(c, hipMemcpyAsync(accum_dev, c->gathered.p, bytes, hipMemcpyDeviceToDevice, s));
+    return RT_OK;
+  }
   int32_t n_total = 0, max_tiles = 0;
   rt_tile_layout(cam, world, &n_total, &max_tiles);
   const int tiles_x = (cam->image_width + kTile - 1) / kTile;
-  HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, launch_unpack(static_cast<const double*>(c->gathered.p), world, max_tiles, n_total, tiles_x,
                            cam->image_width, cam->image_height, accum_dev, s));
+  return RT_OK;
+}
+
+// Every rank's scene digest must be the same: an 8-byte all-gather, read on the host.  All ranks see the
+// same gathered digests, so a mismatch fails on every rank alike (no rank is left waiting in a collective).
+int check_digests(rt_ctx* c, rt_comm* m, hipStream_t s) {
+  const size_t bytes = (size_t)m->world * sizeof(uint64_t);
+  int st = ensure(c, c->digests, bytes + sizeof(uint64_t));
+  if (st) return st;
+  uint64_t* d = static_cast<uint64_t*>(c->digests.p);
+  HIP_TRY(c, hipMemcpyAsync(d + m->world, &c->digest, sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  RCCL_TRY(c, rccl().AllGather(d + m->world, d, 1, ncclUint64, m->comm, s));
+  std::vector<uint64_t> all(m->world);
+  HIP_TRY(c, hipMemcpyAsync(all.data(), d, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  for (int r = 0; r < m->world; ++r)
+    if (all[r] != all[0])
+      return fail(c, RT_E_INVALID, "scene mismatch across ranks: rank %d holds scene %016llx, rank 0 %016llx", r,
+                  (unsigned long long)all[r], (unsigned long long)all[0]);
   return RT_OK;
 }
 
@@ -1554,13 +1758,25 @@ int rt_render_sharded(rt_ctx* c, rt_comm* m, const rt_camera* cam, const rt_rend
   if (!m || !m->comm) return fail(c, RT_E_INVALID, "no communicator");
   if (m->device != c->device) return fail(c, RT_E_INVALID, "communicator of device %d used with device %d", m->device, c->device);
   if (m->rank == 0 && !accum_dev) return fail(c, RT_E_INVALID, "accum_dev is NULL on the root");
+  if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded (call rt_scene_upload first)");
+  if (!p || !cam) return fail(c, RT_E_INVALID, "camera/params is NULL");
+  int part = 0;
+  int st = frame_partition(c, p, m->world, &part);
+  if (st) return st;
   hipStream_t s;
   resolve_stream(c, stream, &s);
+  HIP_TRY(c, hipSetDevice(c->device));
+  if ((st = check_digests(c, m, s))) return st;
   size_t count = 0;
-  int st = shard_render(c, cam, p, m->world, m->rank, s, &count);
-  if (st) return st;
-  RCCL_TRY(c, rccl().Gather(c->packed.p, m->rank == 0 ? c->gathered.p : nullptr, count, ncclFloat64, 0, m->comm, s));
-  if (m->rank == 0) return shard_unpack(c, cam, m->world, accum_dev, s);
+  if ((st = shard_render(c, cam, p, part, m->world, m->rank, s, &count))) return st;
+  if (part == RT_PARTITION_SAMPLES) {
+    RCCL_TRY(c, rccl().AllToAll(c->packed.p, c->parts.p, count, ncclFloat64, m->comm, s));
+    if ((st = shard_band_sum(c, m->world, count, s))) return st;
+    RCCL_TRY(c, rccl().Gather(c->band.p, m->rank == 0 ? c->gathered.p : nullptr, count, ncclFloat64, 0, m->comm, s));
+  } else {
+    RCCL_TRY(c, rccl().Gather(c->packed.p, m->rank == 0 ? c->gathered.p : nullptr, count, ncclFloat64, 0, m->comm, s));
+  }
+  if (m->rank == 0) return shard_unpack(c, cam, part, m->world, accum_dev, s);
   return RT_OK;
 }
 
@@ -1577,8 +1793,16 @@ int rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_camera* cam, const 
     for (int j = 0; j < i; ++j)
       if (devs[j] == devs[i]) return fail(root, RT_E_INVALID, "device %d appears twice", devs[i]);
   }
-  int st = need_rccl(root);
+  for (int i = 0; i < n; ++i) {
+    if (!ctxs[i]->have_scene) return fail(root, RT_E_INVALID, "device %d: no scene uploaded", devs[i]);
+    if (ctxs[i]->digest != root->digest)
+      return fail(root, RT_E_INVALID, "scene mismatch: device %d holds scene %016llx, device %d %016llx", devs[i],
+                  (unsigned long long)ctxs[i]->digest, devs[0], (unsigned long long)root->digest);
+  }
+  int part = 0;
+  int st = frame_partition(root, p, n, &part);
   if (st) return st;
+  if ((st = need_rccl(root))) return st;
   if (root->group_devices != devs) {  // (re)build the communicators of this device set
     for (rt_comm& m : root->group_comms)
       if (m.comm) (void)rccl().CommDestroy(m.comm);
@@ -1589,25 +1813,48 @@ int rt_render_multi(rt_ctx* const* ctxs, int32_t n, const rt_camera* cam, const 
     for (int i = 0; i < n; ++i) root->group_comms.push_back(rt_comm{comms[i], n, i, devs[i]});
     root->group_devices = devs;
   }
-  // every device renders its tiles (asynchronous, all devices at once), then one grouped gather
+  // every device renders its share (asynchronous, all devices at once), then grouped collectives
   std::vector<size_t> count(n);
   for (int i = 0; i < n; ++i) {
-    if ((st = shard_render(ctxs[i], cam, p, n, i, ctxs[i]->stream, &count[i])))
+    if ((st = shard_render(ctxs[i], cam, p, part, n, i, ctxs[i]->stream, &count[i])))
       return i ? fail(root, st, "device %d: %s", devs[i], ctxs[i]->err.c_str()) : st;
   }
-  RCCL_TRY(root, rccl().GroupStart());
-  for (int i = 0; i < n; ++i) {
-    const ncclResult_t r = rccl().Gather(ctxs[i]->packed.p, i == 0 ? root->gathered.p : nullptr, count[i], ncclFloat64, 0,
-                                         root->group_comms[i].comm, ctxs[i]->stream);
-    if (r != ncclSuccess) {
-      (void)rccl().GroupEnd();
-      return fail(root, RT_E_RCCL, "ncclGather (rank %d): %s", i, rccl().GetErrorString(r));
+  auto grouped = [&](auto&& one) -> int {
+    RCCL_TRY(root, rccl().GroupStart());
+    for (int i = 0; i < n; ++i) {
+      const ncclResult_t r = one(i);
+      if (r != ncclSuccess) {
+        (void)rccl().GroupEnd();
+        return fail(root, RT_E_RCCL, "collective (rank %d): %s", i, rccl().GetErrorString(r));
+      }
     }
+    RCCL_TRY(root, rccl().GroupEnd());
+    return RT_OK;
+  };
+  if (part == RT_PARTITION_SAMPLES) {
+    if ((st = grouped([&](int i) {
+           return rccl().AllToAll(ctxs[i]->packed.p, ctxs[i]->parts.p, count[i], ncclFloat64, root->group_comms[i].comm,
+                                  ctxs[i]->stream);
+         })))
+      return st;
+    for (int i = 0; i < n; ++i)
+      if ((st = shard_band_sum(ctxs[i], n, count[i], ctxs[i]->stream))) return i ? fail(root, st, "device %d: %s", devs[i], ctxs[i]->err.c_str()) : st;
+    if ((st = grouped([&](int i) {
+           return rccl().Gather(ctxs[i]->band.p, i == 0 ? root->gathered.p : nullptr, count[i], ncclFloat64, 0,
+                                root->group_comms[i].comm, ctxs[i]->stream);
+         })))
+      return st;
+  } else {
+    if ((st = grouped([&](int i) {
+           return rccl().Gather(ctxs[i]->packed.p, i == 0 ? root->gathered.p : nullptr, count[i], ncclFloat64, 0,
+                                root->group_comms[i].comm, ctxs[i]->stream);
+         })))
+      return st;
   }
-  RCCL_TRY(root, rccl().GroupEnd());
   const size_t bytes = (size_t)cam->image_width * cam->image_height * 3 * sizeof(double);
+  HIP_TRY(root, hipSetDevice(root->device));
   if ((st = ensure(root, root->accum, bytes))) return st;
-  if ((st = shard_unpack(root, cam, n, static_cast<double*>(root->accum.p), root->stream))) return st;
+  if ((st = shard_unpack(root, cam, part, n, static_cast<double*>(root->accum.p), root->stream))) return st;
   HIP_TRY(root, hipMemcpyAsync(accum_host, root->accum.p, bytes, hipMemcpyDeviceToHost, root->stream));
   for (int i = n - 1; i >= 0; --i) {
     HIP_TRY(root, hipSetDevice(ctxs[i]->device));

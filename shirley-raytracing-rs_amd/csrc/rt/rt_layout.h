@@ -196,7 +196,8 @@ struct DWork {
   int32_t tiles_x, tiles_y;      // tile grid of the rendered window (tiles_y rows from ty0)
   int32_t tile_rank, tile_world;
   int32_t n_tiles_rank;          // tiles owned by this rank
-  int32_t samples;               // spp
+  int32_t samples;               // end of the launch's sample range (exclusive): a unit's samples stop here
+  int32_t sample_base;           // first sample of the launch's range: chunk c = samples [base + c chunk, ..)
   int32_t chunk;                 // samples per unit
   int32_t n_chunks;
   int32_t max_depth;

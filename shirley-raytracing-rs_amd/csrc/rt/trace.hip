@@ -279,7 +279,7 @@ void trace_kernel(KParams P) {
         if (px < kc->width && py < kc->height) {
           PH_COUNT(10);
           has_unit = true;
-          const int s0 = chunk * kw->chunk;
+          const int s0 = kw->sample_base + chunk * kw->chunk;
           s_end = min(kw->samples, s0 + kw->chunk);
           rng.sample = (uint32_t)s0 - 1u;  // advanced before each sample (wraps to s0)
           rng.pixel = (uint32_t)py * (uint32_t)kc->width + (uint32_t)px;
@@ -418,10 +418,12 @@ void trace_kernel(KParams P) {
 
 // Sum the per-chunk partials of each pixel in chunk order and write the Image.data layout
 // (row 0 = bottom, image.rs:10-14) or the packed tile layout used by the multi-GPU gather.
+// accumulate: a later sample pass of the same call — the sum starts from the value the earlier passes
+// left in `out` and goes on adding chunks in order, so the additions are exactly one pass's.
 __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ partial, int n_chunks,
                                                      int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
                                                      int tile_world, int width, int row0, int row1, int packed,
-                                                     double* __restrict__ out) {
+                                                     int accumulate, double* __restrict__ out) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long n_pix = (long long)n_tiles_rank * kTilePixels;
   if (i >= n_pix) return;
@@ -432,6 +434,12 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
   int py = (ty0 + (int)(gt / tiles_x)) * kTile + lp / kTile;
   bool inside = px < width && py >= row0 && py < row1;
   double r = 0.0, g = 0.0, b = 0.0;
+  const long long o = packed ? i * 3 : ((long long)(py - row0) * width + px) * 3;
+  if (accumulate && (packed || inside)) {
+    r = out[o + 0];
+    g = out[o + 1];
+    b = out[o + 2];
+  }
   if (inside) {
     for (int c = 0; c < n_chunks; ++c) {
       const double* p = partial + ((long long)c * n_pix + i) * 3;
@@ -440,16 +448,22 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
       b += p[2];
     }
   }
-  if (packed) {
-    out[i * 3 + 0] = r;
-    out[i * 3 + 1] = g;
-    out[i * 3 + 2] = b;
-  } else if (inside) {
-    long long o = ((long long)(py - row0) * width + px) * 3;
+  if (packed || inside) {
     out[o + 0] = r;
     out[o + 1] = g;
     out[o + 2] = b;
   }
+}
+
+// Sample-partitioned frames (RT_PARTITION_SAMPLES): a rank's row band holds one partial band per rank,
+// parts[r][i]; the band's sums are added in rank order (deterministic for any arrival order).
+__global__ __launch_bounds__(256) void sum_parts_kernel(const double* __restrict__ parts, int n_parts, long long n,
+                                                        double* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double s = parts[i];
+  for (int r = 1; r < n_parts; ++r) s += parts[(long long)r * n + i];
+  out[i] = s;
 }
 
 // image.rs:31-44 to_image + color.rs:31-38 to_pixel on the device: per channel c * (1/S), sqrt,
@@ -728,12 +742,20 @@ hipError_t launch_hit4(const DScene& S, bool wide, const double* rays, int n, do
 }
 
 hipError_t launch_reduce(const double* partial, int n_chunks, int n_tiles_rank, int tiles_x, int ty0, int tile_rank,
-                         int tile_world, int width, int row0, int row1, int packed, double* out, hipStream_t stream) {
+                         int tile_world, int width, int row0, int row1, int packed, int accumulate, double* out,
+                         hipStream_t stream) {
   long long n = (long long)n_tiles_rank * kTilePixels;
   int blocks = (int)((n + 255) / 256);
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(reduce_kernel, dim3(blocks), dim3(256), 0, stream, partial, n_chunks, n_tiles_rank, tiles_x,
-                     ty0, tile_rank, tile_world, width, row0, row1, packed, out);
+                     ty0, tile_rank, tile_world, width, row0, row1, packed, accumulate, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_sum_parts(const double* parts, int n_parts, long long n, double* out, hipStream_t stream) {
+  const long long blocks = (n + 255) / 256;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(sum_parts_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, parts, n_parts, n, out);
   return hipGetLastError();
 }
 

@@ -245,7 +245,7 @@ __global__ __launch_bounds__(kTraceThreadsWide, 1) void split_kernel(KParams P) 
         const int py = ty * kTile + (lp / kTile);
         if (px < C.width && py < C.height) {
           has_unit = true;
-          const int s0 = chunk * W.chunk;
+          const int s0 = W.sample_base + chunk * W.chunk;
           s_end = min(W.samples, s0 + W.chunk);
           rng.sample = (uint32_t)s0 - 1u;
           rng.pixel = (uint32_t)py * (uint32_t)C.width + (uint32_t)px;

@@ -456,7 +456,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
         int ppx = tx * kTile + (lp % kTile), ppy = ty * kTile + (lp / kTile);
         if (ppx < C.width && ppy < C.height) {
           pix = (uint32_t)ppy * (uint32_t)C.width + (uint32_t)ppx;
-          s_next = chunk * W.chunk;
+          s_next = W.sample_base + chunk * W.chunk;
           s_end = min(W.samples, s_next + W.chunk);
           st.part[slot] = (unsigned long long)chunk * pix_per_chunk + lt * kTilePixels + (unsigned long long)lp;
           st.sx[slot] = 0.0;

@@ -9,6 +9,6 @@ from .scene import (SceneBuilder, Scene, TextureLoader, Metal, Dielectric, Lambe
                     FairyLight, Sphere, RectBox, xy_rect, yz_rect, xz_rect, SkyBox, Vec3,
                     Isotropic, MovingSphere, ConstantMedium, Transform)
 from .camera import CameraBuilder, CameraPosition, default_camera, cornell_camera, scene_camera  # noqa: F401
-from .render import (Device, RenderSettings, Comm, render_scene, render_multi, comm_unique_id, to_image,  # noqa: F401
+from .render import (Device, RenderSettings, Comm, render_scene, render_multi, comm_unique_id, scene_digest, to_image,  # noqa: F401
                      write_png, tile_layout)
 from . import scenes  # noqa: F401

@@ -25,6 +25,7 @@ RT_BVH_REFERENCE, RT_BVH_SAH = 0, 1
 RT_BVH_NODES_GLOBAL, RT_BVH_NODES_HALF_LDS, RT_BVH_NODES_LDS = 0x100, 0x200, 0x400
 RT_ENGINE_AUTO, RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_SPLIT, RT_ENGINE_TIMING = 0, 1, 2, 3, 0x10
 RT_TRAVERSAL_BINARY, RT_TRAVERSAL_RENDER = 0, 1
+RT_PARTITION_AUTO, RT_PARTITION_TILES, RT_PARTITION_SAMPLES = 0, 1, 2
 
 _d3 = C.c_double * 3
 _d6 = C.c_double * 6
@@ -74,7 +75,10 @@ class rt_camera(C.Structure):
 class rt_render_params(C.Structure):
     _fields_ = [("samples", C.c_int32), ("max_depth", C.c_int32), ("seed", C.c_uint64),
                 ("tile_rank", C.c_int32), ("tile_world", C.c_int32), ("sample_chunk", C.c_int32),
-                ("engine", C.c_int32)]
+                ("engine", C.c_int32),
+                # ABI 6
+                ("sample_begin", C.c_int32), ("sample_count", C.c_int32), ("partition", C.c_int32),
+                ("scratch_mb", C.c_int32)]
 
 
 class rt_scene_stats(C.Structure):
@@ -90,7 +94,9 @@ class rt_counters(C.Structure):
                 ("engine", C.c_int32), ("iterations", C.c_int32), ("slots", C.c_uint64),
                 ("extend_ms", C.c_double), ("shade_ms", C.c_double), ("texture_ms", C.c_double),
                 # ABI 4
-                ("sample_chunk", C.c_int32), ("n_chunks", C.c_int32)]
+                ("sample_chunk", C.c_int32), ("n_chunks", C.c_int32),
+                # ABI 6
+                ("passes", C.c_int32), ("trace_launches", C.c_int32), ("scratch_bytes", C.c_uint64)]
 
 
 class rt_bvh_node(C.Structure):
@@ -119,6 +125,8 @@ RT_SIGNATURES = {
     "rt_last_error": (C.c_char_p, [C.c_void_p]),
     "rt_scene_upload": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_desc), C.c_int32]),
     "rt_scene_stats_get": (C.c_int, [C.c_void_p, C.POINTER(rt_scene_stats)]),
+    "rt_scene_digest": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    "rt_scene_digest_host": (C.c_int, [C.POINTER(rt_scene_desc), C.c_int32, C.POINTER(C.c_uint64)]),
     "rt_render": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params), C.c_void_p]),
     "rt_render_scanlines": (C.c_int, [C.c_void_p, C.POINTER(rt_camera), C.POINTER(rt_render_params),
                                       C.c_int32, C.c_int32, C.c_void_p]),

@@ -59,3 +59,38 @@ def gather_tiles(packed, world: int):
     parts = [torch.empty_like(host) for _ in range(world)]
     dist.all_gather(parts, host)
     return torch.stack(parts).to(packed.device)
+
+
+# ---- sample partition (RT_PARTITION_SAMPLES): the same exchange as rt_render_sharded's -------------
+def sample_share(begin: int, end: int, rank: int, world: int):
+    """Rank `rank`'s part [b, e) of the frame's sample range [begin, end) (rt_api.cpp shard_render)."""
+    n = end - begin
+    return begin + n * rank // world, begin + n * (rank + 1) // world
+
+
+def band_rows(height: int, world: int) -> int:
+    """Rows of one band: rank b owns image rows [b * band_rows, (b + 1) * band_rows)."""
+    return (height + world - 1) // world
+
+
+def reduce_sample_bands(local, world: int):
+    """A rank's whole-frame sums over its samples, [H][W][3] (torch) -> on rank 0 the frame summed over
+    the ranks in rank order (None elsewhere): all-to-all of row bands, the rank-order sum of each band on
+    its owner (sum_parts_kernel), gather of the bands to rank 0 — what rt_render_sharded does with RCCL."""
+    import torch
+    import torch.distributed as dist
+    h, w, _ = local.shape
+    rows = band_rows(h, world)
+    padded = torch.zeros((world * rows, w, 3), dtype=local.dtype, device=local.device)
+    padded[:h] = local
+    parts = torch.empty_like(padded)
+    dist.all_to_all_single(parts.view(-1), padded.view(-1))  # parts[r] = rank r's rows of my band
+    parts = parts.view(world, rows, w, 3)
+    band = parts[0].clone()
+    for r in range(1, world):
+        band += parts[r]
+    bands = [torch.empty_like(band) for _ in range(world)]
+    dist.all_gather(bands, band)
+    if dist.get_rank() != 0:
+        return None
+    return torch.cat(bands)[:h]

@@ -31,15 +31,23 @@ class RenderSettings:
     tile_world: int = 1
     engine: str = "auto"   # auto | megakernel | wavefront | split
     timing: bool = False   # per-launch HIP-event timing of the wavefront kernels (rt_counters *_ms)
+    # ABI 6: samples [sample_begin, sample_begin + sample_count) of the frame (0 = to `samples`)
+    sample_begin: int = 0
+    sample_count: int = 0
+    partition: str = "auto"  # multi-GPU: auto | tiles | samples
+    scratch_mb: int = 0      # partial-sum scratch bound per call in MiB (0 = the library default)
 
     ENGINES = {"auto": N.RT_ENGINE_AUTO, "megakernel": N.RT_ENGINE_MEGAKERNEL, "wavefront": N.RT_ENGINE_WAVEFRONT,
                "split": N.RT_ENGINE_SPLIT}
+    PARTITIONS = {"auto": N.RT_PARTITION_AUTO, "tiles": N.RT_PARTITION_TILES, "samples": N.RT_PARTITION_SAMPLES}
 
     def params(self) -> N.rt_render_params:
         p = N.rt_render_params()
         p.samples, p.max_depth, p.seed = int(self.samples), int(self.max_reflect), int(self.seed)
         p.tile_rank, p.tile_world, p.sample_chunk = int(self.tile_rank), int(self.tile_world), int(self.sample_chunk)
         p.engine = self.ENGINES[self.engine] | (N.RT_ENGINE_TIMING if self.timing else 0)
+        p.sample_begin, p.sample_count = int(self.sample_begin), int(self.sample_count)
+        p.partition, p.scratch_mb = self.PARTITIONS[self.partition], int(self.scratch_mb)
         return p
 
 
@@ -74,6 +82,12 @@ class Device:
         _check(self._h, N.rt_lib().rt_scene_upload(self._h, scene.desc_ptr, builder))
         self.scene = scene
         return self
+
+    def digest(self) -> int:
+        """rt_scene_digest: 64-bit digest of the uploaded scene (the multi-GPU calls compare them)."""
+        d = C.c_uint64()
+        _check(self._h, N.rt_lib().rt_scene_digest(self._h, C.byref(d)))
+        return d.value
 
     def stats(self) -> N.rt_scene_stats:
         s = N.rt_scene_stats()
@@ -186,6 +200,16 @@ def render_multi(devices, camera: N.rt_camera, settings: RenderSettings) -> np.n
     _check(devices[0].handle, N.rt_lib().rt_render_multi(arr, len(devices), C.byref(camera), C.byref(p),
                                                          out.ctypes.data))
     return out
+
+
+def scene_digest(scene: Scene, bvh: str = "reference") -> int:
+    """rt_scene_digest_host: the digest rt_scene_upload would record for this scene (no device needed)."""
+    builder = {"reference": N.RT_BVH_REFERENCE, "sah": N.RT_BVH_SAH}[bvh]
+    d = C.c_uint64()
+    code = N.rt_lib().rt_scene_digest_host(scene.desc_ptr, builder, C.byref(d))
+    if code:
+        raise N.RtError(code, "rt_scene_digest_host: invalid scene")
+    return d.value
 
 
 def tile_layout(camera: N.rt_camera, world: int):

@@ -159,8 +159,9 @@ class SphereScene:
         self.desc_ptr = C.pointer(self.desc)
 
 
-def params(samples, max_depth=50, seed=0x5EED, chunk=0, rank=0, world=1):
+def params(samples, max_depth=50, seed=0x5EED, chunk=0, rank=0, world=1, sample_begin=0, sample_count=0):
     p = N.rt_render_params()
     p.samples, p.max_depth, p.seed = samples, max_depth, seed
     p.sample_chunk, p.tile_rank, p.tile_world = chunk, rank, world
+    p.sample_begin, p.sample_count = sample_begin, sample_count
     return p

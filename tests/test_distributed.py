@@ -71,6 +71,62 @@ def test_two_rank_tile_gather_equals_single_frame(tmp_path, world):
     assert (owned == 1).all()
 
 
+def _range_frame(b, e):
+    """The oracle's frame over samples [b, e) (its render_scanline restatement takes the ABI-6 range)."""
+    import oracle_lib as O
+    import raytracer as rt
+    scene = rt.scenes.random_scene(SEED).finalize(SEED)
+    cam = rt.default_camera(W, "square")
+    cam.image_height = H
+    img, _ = O.OracleScene(scene).render(cam, O.params(SPP_S, 50, SEED, sample_begin=b, sample_count=e - b))
+    return img
+
+
+SPP_S = 5  # the sample-split frame: 5 samples over 2 or 3 ranks (uneven shares)
+
+
+def _sample_worker(rank, world, port, result_path):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(repo, "shirley-raytracing-rs_amd"))
+    sys.path.insert(0, os.path.join(repo, "tests"))
+    import torch
+    import torch.distributed as dist
+    from raytracer import parallel as P
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    b, e = P.sample_share(0, SPP_S, rank, world)
+    local = torch.from_numpy(_range_frame(b, e))
+    out = P.reduce_sample_bands(local, world)
+    if rank == 0:
+        np.save(result_path, out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_split_reduce_equals_rank_order_sum(tmp_path, world):
+    """RT_PARTITION_SAMPLES on CPU ranks: every rank renders all pixels for its share of the samples, the
+    row bands are exchanged (all-to-all), summed in rank order and gathered to rank 0.  The result equals
+    the rank-order sum of the shares bit for bit, and the one-range frame within reassociation
+    (|d| <= 1e-12 |sum|)."""
+    import random
+    from raytracer import parallel as P
+    port = 29500 + random.randint(0, 2000)
+    out = str(tmp_path / "img.npy")
+    mp.spawn(_sample_worker, args=(world, port, out), nprocs=world, join=True)
+    img = np.load(out)
+    shares = [P.sample_share(0, SPP_S, r, world) for r in range(world)]
+    assert shares[0][0] == 0 and shares[-1][1] == SPP_S
+    assert all(shares[r][1] == shares[r + 1][0] for r in range(world - 1))
+    want = _range_frame(*shares[0])
+    for b, e in shares[1:]:
+        want = want + _range_frame(b, e)
+    assert np.array_equal(img, want)
+    full = _range_frame(0, SPP_S)
+    assert np.all(np.abs(img - full) <= 1e-12 * np.abs(full) + 1e-300)
+
+
 def test_tile_layout_matches_device_abi():
     import raytracer as rt
     from raytracer import parallel as P

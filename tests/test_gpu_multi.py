@@ -116,3 +116,25 @@ def test_bench_sharded_config5_leg(gpu):
     finally:
         comm.close()
         dist.destroy_process_group()
+
+
+def test_bench_gpus_flag_on_this_box():
+    """bench.py --gpus: 1 runs the single-process bench as before (n_gpus 1, the to-host step time next
+    to the device-only one); more ranks than this box's GPUs exit non-zero with a message instead of
+    printing a line labelled with the wrong GPU count."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import torch
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    base = [sys.executable, os.path.join(repo, "bench.py"), "--steps", "2", "--warmup", "1", "--width", "64",
+            "--spp", "4", "--no-cpu", "--no-configs"]
+    r = subprocess.run(base + ["--gpus", "1"], capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith('{"metric"')][-1])
+    assert line["n_gpus"] == 1 and line["config"]["ranks"] == 1 and line["steps"] == 2
+    assert line["ms_per_step"] >= line["device_ms_per_step"] > 0
+    n = torch.cuda.device_count()
+    r = subprocess.run(base + ["--gpus", str(n + 1)], capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode != 0 and "visible GPU" in r.stderr

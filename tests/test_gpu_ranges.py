@@ -1,0 +1,155 @@
+"""ABI 6 on the GPU: the sample range of rt_render_params ("tile rect / sample range"),
+the sample passes that bound the partial-sum scratch, the sample partition of the multi-GPU calls and the
+scene-digest check (reference: the per-pixel sample loop, /root/reference/src/raytracer/render.rs:58-69).
+
+* A range [b, e) renders exactly the samples b..e-1 of every pixel: with sample_chunk >= e - b its
+  per-pixel sums equal the oracle's in-order sums over the same range (the oracle's render_scanline
+  restatement takes the same range), within the module tolerance of test_gpu_parity.py.
+* Splitting [0, S) into ranges changes only the order of additions: sum([0,k)) + sum([k,S)) equals the
+  one-call frame within |d| <= 1e-12 |sum| per channel (REASSOC below).
+* Sample passes keep every per-pixel addition and its order (reduce_kernel `accumulate`): frames are
+  bit-identical for every scratch bound.
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import raytracer as rt
+from test_gpu_parity import check_parity, EXACT_MIN
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED
+REASSOC = 1e-12  # relative per-channel bound of a reassociated sum
+
+
+def _reassoc_close(a, b):
+    assert a.shape == b.shape
+    assert np.all(np.abs(a - b) <= REASSOC * np.maximum(np.abs(a), np.abs(b)) + 1e-300), \
+        f"max rel diff {np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-300)):.3g}"
+
+
+@pytest.fixture(scope="module")
+def random_scene():
+    return rt.scenes.random_scene(SEED).finalize(SEED)
+
+
+@pytest.mark.parametrize("engine", ["megakernel", "wavefront", "split"])
+def test_range_matches_oracle_range(gpu, random_scene, engine):
+    spp, b, n = 12, 5, 4  # samples [5, 9) of a 12-spp frame
+    cam = rt.default_camera(40, "std16x9")
+    gpu.upload(random_scene)
+    got = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=n, sample_begin=b, sample_count=n,
+                                            engine=engine))
+    want, ocnt = O.OracleScene(random_scene).render(cam, O.params(spp, 50, SEED, sample_begin=b, sample_count=n))
+    check_parity(got, want, n, frac_exact=EXACT_MIN["random"])
+    c = gpu.counters()
+    assert c.samples == cam.image_width * cam.image_height * n == ocnt.samples
+
+
+def test_ranges_sum_to_the_frame(gpu, random_scene):
+    spp = 24
+    cam = rt.default_camera(48, "std16x9")
+    gpu.upload(random_scene)
+    s = dict(samples=spp, seed=SEED, sample_chunk=4)
+    full = gpu.render(cam, rt.RenderSettings(**s))
+    a = gpu.render(cam, rt.RenderSettings(**s, sample_begin=0, sample_count=8))
+    b = gpu.render(cam, rt.RenderSettings(**s, sample_begin=8))  # count 0: to the end
+    _reassoc_close(a + b, full)
+    # chunk-aligned ranges render the frame's own units: the first range's chunk sums are the frame's
+    # first two chunk sums, so a frame whose chunks are summed in that order is exact
+    c0 = gpu.render(cam, rt.RenderSettings(**s, sample_begin=0, sample_count=4))
+    c1 = gpu.render(cam, rt.RenderSettings(**s, sample_begin=4, sample_count=4))
+    assert np.array_equal(c0 + c1, a)
+    # an empty range is an all-zero frame; a range beyond the frame is refused
+    z = gpu.render(cam, rt.RenderSettings(**s, sample_begin=spp))
+    assert not z.any() and gpu.counters().samples == 0
+    with pytest.raises(rt.RtError, match="sample range"):
+        gpu.render(cam, rt.RenderSettings(**s, sample_begin=20, sample_count=5))
+    with pytest.raises(rt.RtError, match="sample range"):
+        gpu.render(cam, rt.RenderSettings(**s, sample_begin=-1))
+
+
+@pytest.mark.parametrize("engine", ["megakernel", "wavefront", "split"])
+def test_sample_passes_are_bit_identical(gpu, random_scene, engine):
+    """scratch_mb = 1 cuts a 64x64 @ 40 spp frame with 1-sample units (98 KB of partials per chunk) into
+    4 passes of 10 chunks; the frame is bit-identical to the one-pass frame and the counters add up."""
+    cam = rt.default_camera(64, "square")
+    gpu.upload(random_scene)
+    s = dict(samples=40, seed=SEED, sample_chunk=1, engine=engine)
+    one = gpu.render(cam, rt.RenderSettings(**s))
+    c1 = gpu.counters()
+    assert c1.passes == 1 and c1.n_chunks == 40
+    many = gpu.render(cam, rt.RenderSettings(**s, scratch_mb=1))
+    c4 = gpu.counters()
+    assert c4.passes == 4 and c4.trace_launches == 4 and c4.scratch_bytes <= (1 << 20)
+    assert np.array_equal(one, many)
+    assert c4.samples == c1.samples and c4.segments == c1.segments
+    # the same through a sample range and the packed tile layout
+    r1 = gpu.render(cam, rt.RenderSettings(**s, sample_begin=7, sample_count=29))
+    r4 = gpu.render(cam, rt.RenderSettings(**s, sample_begin=7, sample_count=29, scratch_mb=1))
+    assert gpu.counters().passes == 3
+    assert np.array_equal(r1, r4)
+
+
+def _sample_split(gpu, cam, settings, world):
+    """RT_PARTITION_SAMPLES simulated on one device: rank r renders all pixels for its share of the
+    frame's samples; the per-rank frames are summed in rank order (what the band sum computes)."""
+    spp = settings["samples"]
+    parts = []
+    for r in range(world):
+        b, e = spp * r // world, spp * (r + 1) // world
+        if e > b:
+            parts.append(gpu.render(cam, rt.RenderSettings(**settings, sample_begin=b, sample_count=e - b)))
+        else:
+            parts.append(np.zeros((cam.image_height, cam.image_width, 3)))
+    out = parts[0].copy()
+    for p in parts[1:]:
+        out += p
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sample_split_equals_frame_within_reassociation(gpu, random_scene, world):
+    cam = rt.default_camera(40, "std16x9")
+    gpu.upload(random_scene)
+    s = dict(samples=20, seed=SEED, sample_chunk=20)
+    full = gpu.render(cam, rt.RenderSettings(**s))
+    _reassoc_close(_sample_split(gpu, cam, s, world), full)
+
+
+@pytest.mark.parametrize("partition", ["samples", "tiles"])
+def test_multi_one_device_partitions(gpu, random_scene, partition):
+    """rt_render_multi and rt_render_sharded with either partition on a one-rank communicator: the
+    digest check, the render, the exchange (all-to-all + band sum + gather, or the tile gather) all run,
+    and the frame equals rt_render's bit for bit (one rank renders everything)."""
+    import torch
+    cam = rt.default_camera(53, "std16x9")
+    gpu.upload(random_scene, "sah")
+    s = rt.RenderSettings(samples=5, seed=SEED, partition=partition)
+    want = gpu.render(cam, s)
+    assert np.array_equal(rt.render_multi([gpu], cam, s), want)
+    comm = gpu.comm_init_rank(rt.comm_unique_id(), 1, 0)
+    try:
+        stream = torch.cuda.current_stream().cuda_stream
+        a = torch.full((cam.image_height, cam.image_width, 3), -1.0, dtype=torch.float64, device="cuda")
+        gpu.render_sharded(comm, cam, s, a.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(a.cpu().numpy(), want)
+        # a sample range is the frame's: the partition splits it
+        s2 = rt.RenderSettings(samples=5, seed=SEED, partition=partition, sample_begin=1, sample_count=3)
+        gpu.render_sharded(comm, cam, s2, a.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(a.cpu().numpy(), gpu.render(cam, s2))
+    finally:
+        comm.close()
+
+
+def test_scene_digest_on_device(gpu, random_scene):
+    gpu.upload(random_scene, "sah")
+    d = gpu.digest()
+    assert d == rt.scene_digest(random_scene, "sah")
+    gpu.upload(random_scene, "sah")
+    assert gpu.digest() == d
+    gpu.upload(rt.scenes.create_cornell_box().finalize(SEED), "sah")
+    assert gpu.digest() != d

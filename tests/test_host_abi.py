@@ -16,6 +16,7 @@ import raytracer as rt
 from raytracer import _native as N
 
 REPO = O.REPO
+SEED = 0x5EED
 
 
 def header_functions(path):
@@ -249,3 +250,31 @@ def test_multi_gpu_entry_points_reject_bad_arguments_without_a_device():
     assert lib.rt_comm_init_rank(None, None, 1, 0, None) == N.RT_E_INVALID
     assert lib.rt_comm_destroy(None) == N.RT_OK
     assert lib.rt_comm_unique_id(None) == N.RT_E_INVALID
+
+
+def test_scene_digest_is_stable_and_discriminating():
+    """rt_scene_digest_host (ABI 6): the digest rt_scene_upload records and the multi-GPU calls compare
+    across ranks — equal for equal scenes (rebuilt from scratch), different for any other scene, seed,
+    material or builder."""
+    a = rt.scenes.random_scene(SEED).finalize(SEED)
+    d = rt.scene_digest(a, "sah")
+    assert d == rt.scene_digest(a, "sah")
+    assert d == rt.scene_digest(rt.scenes.random_scene(SEED).finalize(SEED), "sah")
+    assert d != rt.scene_digest(a, "reference")
+    assert d != rt.scene_digest(rt.scenes.random_scene(SEED + 1).finalize(SEED + 1), "sah")
+    assert d != rt.scene_digest(rt.scenes.random_scene(SEED).finalize(SEED + 1), "sah")  # Perlin tables only
+    assert d != rt.scene_digest(rt.scenes.random_scene(SEED, night=True).finalize(SEED), "sah")
+    digests = {rt.scene_digest(rt.SceneBuilder.builtin(n, SEED).finalize(SEED)) for n in
+               ("random", "demo", "perlin", "earth", "box-light", "cornell", "final:4:30")}
+    assert len(digests) == 7
+    # a one-field change of one object
+    b = rt.scenes.random_scene(SEED).finalize(SEED)
+    b.desc_ptr.contents.objects[3].p[3] += 1e-9
+    assert rt.scene_digest(b, "sah") != d
+
+
+def test_render_params_abi6_layout():
+    import ctypes as C
+    assert C.sizeof(N.rt_render_params) == 48
+    assert N.rt_render_params.sample_begin.offset == 32 and N.rt_render_params.scratch_mb.offset == 44
+    assert C.sizeof(N.rt_counters) == 112

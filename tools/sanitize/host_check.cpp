@@ -14,6 +14,7 @@
 //
 // usage: host_check <asset_dir> <n_mutants> [seed]
 #include <cinttypes>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -74,9 +75,11 @@ int exercise(const sh_scene* s, uint64_t seed, int w, int spp, bool big_ok) {
     }
   }
   rt::BuiltTree ref = rt::build_reference_tree(boxes);
-  rt::BuiltTree sah = rt::build_sah_tree(boxes);
+  rt::BuiltTree sah = rt::build_sah_tree(boxes, false);  // 32-bin SAH
+  rt::BuiltTree sweep = rt::build_sah_tree(boxes, true);  // exact-sweep SAH (the RT_BVH_SAH default)
   (void)rt::tree_branch_depth(ref);
   (void)rt::tree_branch_depth(sah);
+  (void)rt::tree_branch_depth(sweep);
   int rc = 0;
   if (big_ok || v->n_objects <= 4000) {
     or_scene* os = or_scene_new(v);
@@ -203,6 +206,34 @@ int main(int argc, char** argv) {
     if (sh_scene_from_json(e, &s) == 0 && s) {
       exercise(s, 1, 4, 1, false);
       sh_scene_free(s);
+    }
+  }
+  {  // boxes whose centroids are NaN (opposite infinite planes, NaN planes) or infinite, mixed with
+     // ordinary ones: every builder must terminate and place each object in exactly one leaf (the
+     // sweep builder's sort needs a strict weak ordering for that)
+    const double inf = INFINITY, nan = NAN;
+    std::vector<rt::Box> boxes;
+    for (int i = 0; i < 64; ++i) {
+      rt::Box b;
+      for (int k = 0; k < 3; ++k) {
+        const double c = (double)((i * 37 + k * 11) % 17);
+        b.mn[k] = c;
+        b.mx[k] = c + 1.0;
+      }
+      switch (i % 5) {
+        case 1: b.mn[i % 3] = -inf; b.mx[i % 3] = inf; break;  // centroid NaN
+        case 2: b.mn[(i + 1) % 3] = nan; break;               // NaN plane
+        case 3: b.mn[i % 3] = inf; b.mx[i % 3] = inf; break;   // centroid +inf
+        default: break;
+      }
+      boxes.push_back(b);
+    }
+    for (int which = 0; which < 3; ++which) {
+      const rt::BuiltTree t = which == 0 ? rt::build_reference_tree(boxes) : rt::build_sah_tree(boxes, which == 2);
+      std::vector<int> seen(boxes.size(), 0);
+      for (const rt::BuildNode& n : t.nodes)
+        if (n.leaf >= 0 && n.leaf < (int)boxes.size()) seen[n.leaf]++;
+      for (size_t i = 0; i < seen.size(); ++i) CHECK(seen[i] == 1, "builder %d: object %zu in %d leaves", which, i, seen[i]);
     }
   }
   {  // nesting far beyond the recursion limit must be an error, not a stack overflow
