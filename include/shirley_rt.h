@@ -174,8 +174,8 @@ typedef struct rt_render_params {
                          * Automatic usually picks chunk < samples: each chunk is summed in order, then the
                          * chunk sums in chunk order — not render.rs:58-69's single running sum, so the
                          * frame differs from the in-order one by reassociation only (|d| <= 1e-12 |sum|,
-                         * DESIGN.md §2).  The megakernel indexes work units (pixels x ceil(spp / chunk)) in 32 bits: an
-                         * explicit chunk giving >= 2^32 units fails with RT_E_UNSUPPORTED (auto raises it).
+                         * DESIGN.md §2).  The megakernel indexes a launch's work units (pixels x chunks) in 32 bits: a
+                         * call with more runs in several sample passes (see scratch_mb).
                          * The automatic length depends on the pixels a call renders (its tiles) and on
                          * the device's CU count, so tile-sharded frames at different world sizes sum each
                          * pixel's chunks differently (bits differ within the reassociation bound); pass an

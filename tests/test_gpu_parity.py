@@ -360,9 +360,12 @@ def test_edge_cases(gpu, engine):
         gpu.render(cam, rt.RenderSettings(engine=engine, samples=-1))
     with pytest.raises(rt.RtError):
         gpu.render_scanlines(cam, rt.RenderSettings(engine=engine, samples=1), 5, 100)
-    if engine in ("megakernel", "split"):  # 64 pixels x (2^26 + 1) one-sample units >= 2^32: refused before any work
-        with pytest.raises(rt.RtError, match="2\\^32"):
-            gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1))
+    if engine in ("megakernel", "split"):
+        # 64 pixels x (2^26 + 1) one-sample units >= 2^32: the megakernel indexes a launch's units in 32 bits,
+        # so the call runs in two sample passes (ABI 6) instead of being refused
+        big = gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1, max_reflect=1))
+        c = gpu.counters()
+        assert c.passes == 2 and c.samples == 64 * ((1 << 26) + 1) and np.isfinite(big).all()
 
 
 @pytest.mark.parametrize("engine", ENGINES)
