@@ -975,7 +975,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     PH_COUNT(3);
     RT_STAT(++ptests);
     if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) continue;
+#ifndef RT_EXP_NO_SPHERE_BOX  // (timing experiment only: drops the reference's box test)
     if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
+#endif
     t_best = t; best = leaf; face_best = -1; hit = true;
   }
 #pragma unroll 1

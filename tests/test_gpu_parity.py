@@ -361,11 +361,13 @@ def test_edge_cases(gpu, engine):
     with pytest.raises(rt.RtError):
         gpu.render_scanlines(cam, rt.RenderSettings(engine=engine, samples=1), 5, 100)
     if engine in ("megakernel", "split"):
-        # 64 pixels x (2^26 + 1) one-sample units >= 2^32: the megakernel indexes a launch's units in 32 bits,
-        # so the call runs in two sample passes (ABI 6) instead of being refused
+        # 64 pixels x (2^26 + 1) one-sample units (>= 2^32: more than a launch indexes in 32 bits): the call
+        # runs in sample passes (ABI 6) of <= 512 MiB of partial sums — 349525 chunks of 64 pixels each, 193
+        # passes — instead of being refused
         big = gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1, max_reflect=1))
         c = gpu.counters()
-        assert c.passes == 2 and c.samples == 64 * ((1 << 26) + 1) and np.isfinite(big).all()
+        assert c.passes == 193 and c.scratch_bytes <= 512 << 20
+        assert c.samples == 64 * ((1 << 26) + 1) and np.isfinite(big).all()
 
 
 @pytest.mark.parametrize("engine", ENGINES)
