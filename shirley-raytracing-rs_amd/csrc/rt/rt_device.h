@@ -203,6 +203,12 @@ __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t
 // ------------------------------------------------------------------------------------------
 // intersection (t only during traversal; the full hit record is rebuilt for the winner)
 // ------------------------------------------------------------------------------------------
+// (A/B switch) node visits derive the hit-leaf mask from the box compares themselves (RT_VISIT_HC = 1)
+// instead of re-testing the keys' bits
+#ifndef RT_VISIT_HC
+#define RT_VISIT_HC 0
+#endif
+// ------------------------------------------------------------------------------------------
 // aabb.rs:62-79 hit2, per axis: t0 = (min - o) * inv, t1 = (max - o) * inv, swapped when inv < 0,
 // t_min = t0 > t_min ? t0 : t_min, t_max = t1 < t_max ? t1 : t_max, miss when t_max <= t_min
 // (evaluated without the per-axis early exit: t_min only grows and t_max only shrinks, so the final
@@ -826,7 +832,9 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) { return __bu
 // both out (node4_visit).
 template <bool M1, class N4>
 __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3 inv, float tminf, float tmaxf,
-                                           double t_min, double t_max, float& k0, float& k1, float& k2, float& k3) {
+                                           double t_min, double t_max, float& k0, float& k1, float& k2, float& k3,
+                                           const int4& ch, unsigned (&hc)[4]) {
+  const unsigned chw[4] = {(unsigned)ch.x, (unsigned)ch.y, (unsigned)ch.z, (unsigned)ch.w};
   // the near / far plane rows picked per ray by the sign of 1/d (see DNode4F / DNode4C): for 1/d >= 0, fma(lo, i, -o i) <= fma(hi, i, -o i) (the FMA rounds monotonically), so the
   // pick equals the min / max of the two and each child needs only max3 / min3; a NaN (0 * inf) is
   // dropped by max3 / min3 like by the min / max form; an inverted box (lo > hi) now fails, which the
@@ -866,6 +874,7 @@ __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3
     for (int e = 0; e < 2; ++e) {
       const float tn = fmaxf(fmaxf(x0[e], y0[e]), fmaxf(z0[e], tminf));
       const float tf = fminf(fminf(x1[e], y1[e]), fminf(z1[e], tmaxf));
+      hc[2 * h + e] = tn <= tf ? chw[2 * h + e] : 0u;  // the child word where its box is hit (RT_VISIT_HC)
       key[2 * h + e] = tn <= tf ? tn : (M1 ? __uint_as_float(~0u) : __builtin_inff());
     }
   }
@@ -888,6 +897,7 @@ __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3
         tn = fmax(tn, fmin(t0, t1));
         tf = fmin(tf, fmax(t0, t1));
       }
+      hc[k] = tn <= tf ? chw[k] : 0u;
       key[k] = tn <= tf ? __double2float_rd(tn) : (M1 ? __uint_as_float(~0u) : __builtin_inff());
     }
   }
@@ -1050,12 +1060,19 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const N4* lds_n
   ch = *reinterpret_cast<const int4*>(nd.child);
   const float tminf = fmaxf(__double2float_rd(t_min), 1.17549435e-38f);  // entry keys > 0
   constexpr bool kM1 = MODE == kNodesLds || MODE == kSceneLds;
-  node4_keys<kM1>(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3);
+  unsigned hc[4];
+  node4_keys<kM1>(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3, ch, hc);
   RT_STAT(visits += 4);
+#if RT_VISIT_HC
+  // hit leaf: the child word where the box test passed (the key's own compare, no second test), else 0;
+  // its sign bit marks a leaf, gathered into the spread mask
+  return top_bytes(hc[0], hc[1], hc[2], hc[3]) & 0x80808080u;
+#endif
   // hit leaf: key < inf (bits(k) + 0x80800000 keeps the sign bit exactly for bits(k) < bits(inf); keys
   // are >= 0) and a negative child word; as a spread mask
   // (an M1 miss key ~0u: its sum keeps the top bit, so it is masked by ~bits(k) — one v_bitop3 with the
   // child)
+#if !RT_VISIT_HC
   const unsigned m0 = kM1 ? ~__float_as_uint(k0) : ~0u, m1 = kM1 ? ~__float_as_uint(k1) : ~0u;
   const unsigned m2 = kM1 ? ~__float_as_uint(k2) : ~0u, m3 = kM1 ? ~__float_as_uint(k3) : ~0u;
   const unsigned h0 = (__float_as_uint(k0) + 0x80800000u) & m0 & (unsigned)ch.x;
@@ -1063,6 +1080,7 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const N4* lds_n
   const unsigned h2 = (__float_as_uint(k2) + 0x80800000u) & m2 & (unsigned)ch.z;
   const unsigned h3 = (__float_as_uint(k3) + 0x80800000u) & m3 & (unsigned)ch.w;
   return top_bytes(h0, h1, h2, h3) & 0x80808080u;
+#endif
 }
 // visit4's ordering part: internal children as packed words (a miss, k = inf or ~0u, packs above any
 // bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.

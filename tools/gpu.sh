@@ -13,6 +13,13 @@
 #   prof[:bench.py args]     rocprofv3 --kernel-trace --stats (kernel_stats.csv under <tag>/prof)
 #   pmc:<COUNTERS>[:args]    one rocprofv3 --pmc pass (counters comma-separated, one block's limits)
 #   py:<script> [args]       a python tool (e.g. "py:tools/shard_balance.py gpurun_out/x/shard.json")
+# Recipes (profiles/<round>/ evidence):
+#   kernel stats + HBM traffic:  prof pmc:FETCH_SIZE pmc:WRITE_SIZE, then
+#                                python tools/pmc_traffic.py gpurun_out/<tag> profiles/<round> "<workload>" sah
+#   VALU issue / lane use:       "pmc:SQ_WAVE_CYCLES,SQ_ACTIVE_INST_VALU,SQ_INSTS_VALU,SQ_THREAD_CYCLES_VALU,
+#                                SQ_INSTS_VALU_ADD_F64,SQ_INSTS_VALU_MUL_F64,SQ_INSTS_VALU_FMA_F64,SQ_INSTS_SALU:
+#                                --steps 1 --warmup 0 --no-cpu --no-configs", then
+#                                python tools/pmc_valu.py profiles/<round> 4 gpurun_out/<tag>/pmc_SQ_WAVE_CYCLES_...
 # Examples:
 #   gpurun -- 'bash tools/gpu.sh r03a tests smoke "bench:--steps 5" "prof:--steps 3 --no-cpu --no-configs"'
 #   gpurun -- 'bash tools/gpu.sh r03b "ab:main||;f32s||;main||;f32s||"'
@@ -78,6 +85,7 @@ for step in "$@"; do
       pargs=""
       [ "$counters" != "$args" ] && pargs=${args#*:}
       d="$out/pmc_$(echo "$counters" | tr ',' '_')"
+      log="$d.log"  # (tools/pmc_valu.py reads the pass's bench line from <pass dir>.log)
       timeout -s KILL 300 rocprofv3 --pmc $(echo "$counters" | tr ',' ' ') --output-format csv -d "$d" -o run -- \
         python3 bench.py ${pargs:---steps 1 --warmup 0 --no-cpu --no-configs} > "$log" 2>&1
       rc=$?; echo "[$n pmc $counters] rc=$rc"

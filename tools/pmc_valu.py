@@ -1,8 +1,9 @@
 """Summarise the VALU PMC passes of one trace_kernel dispatch into profiles/valu.json (read by bench.py).
 
-Inputs: rocprofv3 --pmc pass directories (tools/profile_valu.sh) whose bench run printed its JSON line
-to <pass>.log.  Each pass profiles ONE frame (bench --steps 1 --warmup 0), so every pass holds exactly
-one trace_kernel dispatch of the same deterministic workload (same seed -> same segments).
+Inputs: rocprofv3 --pmc pass directories (tools/gpu.sh `pmc:` steps) whose bench run printed its JSON line
+to <pass dir>.log.  Each pass profiles ONE frame (bench --steps 1 --warmup 0): the trace_kernel dispatches
+of that frame (one per sample pass) are summed, and every pass sees the same deterministic workload
+(same seed -> same segments).
 
   busy_frac   = SQ_ACTIVE_INST_VALU / (SQ_WAVE_CYCLES / waves_per_simd)   (SIMD issue slots used by VALU)
   lane_util   = SQ_THREAD_CYCLES_VALU / (64 * SQ_ACTIVE_INST_VALU)        (active lanes per VALU cycle)
@@ -20,12 +21,11 @@ import sys
 def dispatch_counters(pass_dir):
     f = glob.glob(os.path.join(pass_dir, "**", "*counter_collection.csv"), recursive=True)[0]
     rows = [r for r in csv.DictReader(open(f)) if "trace_kernel" in r["Kernel_Name"]]
-    ids = sorted({r["Dispatch_Id"] for r in rows})
-    assert len(ids) == 1, f"{pass_dir}: expected one trace_kernel dispatch, got {ids}"
+    ids = sorted({r["Dispatch_Id"] for r in rows}, key=int)
     agg = {}
     for r in rows:
         agg[r["Counter_Name"]] = agg.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-    return f, rows, agg, ids[0]
+    return f, rows, agg, ids
 
 
 def bench_line(pass_dir):
@@ -47,9 +47,10 @@ def main(dst, waves_per_simd, *passes):
             w.writeheader()
             w.writerows(rows)
         b = bench_line(p)
-        segs.add(b["roofline"]["segments_per_launch"])
+        assert len(did) == b["roofline"].get("launches_per_step", 1), f"{p}: dispatches {did} vs the frame's launches"
+        segs.add(b["roofline"]["segments_per_launch"] * b["roofline"].get("launches_per_step", 1))
         cfg = b["config"]
-        sources.append(f"{os.path.basename(out)} (dispatch {did})")
+        sources.append(f"{os.path.basename(out)} (dispatches {','.join(did)})")
     assert len(segs) == 1, f"passes saw different workloads: {segs}"
     seg = segs.pop()
     wps = float(waves_per_simd)

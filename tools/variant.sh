@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build an experiment variant of libshirley_rt.so into exp/<name>/ (for tools/ab2.sh).
+# Build an experiment variant of libshirley_rt.so into exp/<name>/ (for tools/gpu.sh ab steps).
 # Usage: tools/variant.sh <name> [extra hipcc flags...]   e.g. tools/variant.sh phase -DRT_PHASE_TIMING
 # The tree is copied, so a variant can also be made from edited sources: set SRC=<dir> (default: the
 # in-tree package).  LICM_FLAG= (empty) builds without -disable-machine-licm; TRK_FLAG=<flags> adds scheduler flags.
