@@ -448,6 +448,7 @@ float round_up(double x) {
 struct Inflation {
   double delta;
   float origin_limit;
+  double box_bound;  // B: the largest finite |plane| of any box
 };
 Inflation inflation_for(const BuiltTree& t) {
   double B = 0.0;
@@ -457,7 +458,7 @@ Inflation inflation_for(const BuiltTree& t) {
       if (std::isfinite(n.box.mx[k])) B = std::max(B, std::fabs(n.box.mx[k]));
     }
   const double L = std::max(16.0, 4.0 * B);
-  return Inflation{std::ldexp(L + B, -20), (float)L};
+  return Inflation{std::ldexp(L + B, -20), (float)L, B};
 }
 
 // child slot of a 4-wide node: an empty slot never passes (lo = +inf > hi = -inf); a box with a
@@ -1129,6 +1130,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     // a sphere's 1 / radius (sphere.rs:48 `scale(1.0 / self.radius)`), the same IEEE quotient the device
     // would compute per hit record; p[4] is otherwise unused by spheres
     if (q.kind == kPrimSphere || q.kind == kPrimMovingSphere) q.p[4] = 1.0 / q.p[3];
+    // a sphere's inner radius for the box test's fast accept (rt_device.h leaf_tests4): r - 2 m, m =
+    // 2^-46 (B + L) with B the largest box plane and L the origin bound of the f32 node test (the
+    // rounding of this subtraction, <= 2^-53 r, stays far inside the second m)
+    if (q.kind == kPrimSphere) q.p[5] = q.p[3] - 2.0 * std::ldexp(infl.box_bound + (double)infl.origin_limit, -46);
     q.material = o.material | (d->materials[o.material].kind == RT_MAT_DIELECTRIC ? kPrimMatDielectric : 0);
     if (is_extended(o)) {
       if (exts.size() >= (1u << (31 - kPrimExtShift)))

@@ -288,8 +288,8 @@ __device__ __forceinline__ double div_by(double n, const Recip& R, bool ok) {
   return n / R.b;
 }
 __device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Recip& ra, bool ra_ok, double t_min,
-                                           double t_max, double& t) {
-  v3 oc = o - V(p[0], p[1], p[2]);
+                                           double t_max, double& t, v3& oc) {
+  oc = o - V(p[0], p[1], p[2]);
   double half_b = dot(oc, d);
   double c = len2(oc) - p[3] * p[3];
   double disc = half_b * half_b - ra.b * c;
@@ -956,9 +956,13 @@ __device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned
   return __builtin_amdgcn_perm(w1, w0, 0x0c0c0703u) | __builtin_amdgcn_perm(w3, w2, 0x07030c0cu);
 }
 
+// (A/B switch) a sphere hit skips the exact test of its bounding box where that test provably passes
+#ifndef RT_SPHERE_FAST_ACCEPT
+#define RT_SPHERE_FAST_ACCEPT 0
+#endif
 template <int MODE, bool EXT>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
-                                            RaySigns ns, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
+                                            RaySigns ns, bool fast, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, const int32_t* chp, double& t_best, float& tmaxf, int& best,
                                             int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
   // lm: spread mask of hit leaf children (bit 8 i + 7: child i).  A leaf's child word is
@@ -984,8 +988,17 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double t;
     PH_COUNT(3);
     RT_STAT(++ptests);
-    if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) continue;
-#ifndef RT_EXP_NO_SPHERE_BOX  // (timing experiment only: drops the reference's box test)
+    v3 oc;
+    if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t, oc)) continue;
+#if RT_SPHERE_FAST_ACCEPT
+    // The box test passes for sure when the hit point o + t d lies strictly inside the sphere's box by
+    // the scene's margin on every axis and t_min < t < t_best (then every FP slab entry
+    // is < t and every exit > t); p[5] = r - margin (host, <= 0 for a negative radius: never sure).  The
+    // check only decides whether the exact test runs; a lane it does not clear runs slab_sphere.
+    const bool sure = fast && t > t_min && t < t_best && fabs(fma(t, d.x, oc.x)) < pr.p[5] &&
+                      fabs(fma(t, d.y, oc.y)) < pr.p[5] && fabs(fma(t, d.z, oc.z)) < pr.p[5];
+    if (!sure && !slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
+#elif !defined(RT_EXP_NO_SPHERE_BOX)  // (timing experiment only: drops the reference's box test)
     if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
 #endif
     t_best = t; best = leaf; face_best = -1; hit = true;
@@ -1129,7 +1142,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<E
                                         visits, chp);
   if (lm) PH_COUNT(1);
   if (lm)
-    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
+    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, rf.fast, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
                            face_best, rk, seed, ptests);
   return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
 }

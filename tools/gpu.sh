@@ -5,6 +5,7 @@
 #
 # Steps (an argument "name" or "name:args", args split on blanks):
 #   tests[:pytest args]      pytest -m gpu (default: the whole suite; e.g. "tests:tests/test_gpu_ranges.py")
+#   testsv:<variant>[:args]  the same against exp/<variant>'s libraries (SHIRLEY_LIB_DIR)
 #   smoke                    __graft_entry__.smoke()
 #   bench[:bench.py args]    one bench line (default: the driver's defaults)
 #   ab:<spec>;<spec>;...     interleaved A/B, one bench line per spec "variant|ENV=V ...|bench flags"
@@ -52,6 +53,13 @@ for step in "$@"; do
       timeout -k 10 900 python -u -m pytest ${args:-tests} -m gpu -x -v --timeout 120 --timeout-method thread \
         -p no:cacheprovider > "$log" 2>&1
       rc=$?; echo "[$n tests] rc=$rc $(tail -1 "$log")" ;;
+    testsv)  # testsv:<variant>[:pytest args] — the GPU tests against exp/<variant>'s libraries
+      v=${args%%:*}
+      targs=""
+      [ "$v" != "$args" ] && targs=${args#*:}
+      SHIRLEY_LIB_DIR=$PWD/exp/$v timeout -k 10 900 python -u -m pytest ${targs:-tests} -m gpu -x -v --timeout 120 \
+        --timeout-method thread -p no:cacheprovider > "$log" 2>&1
+      rc=$?; echo "[$n tests on exp/$v] rc=$rc $(tail -1 "$log")" ;;
     smoke)
       timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1
       rc=$?; echo "[$n smoke] rc=$rc $(tail -1 "$log")" ;;
