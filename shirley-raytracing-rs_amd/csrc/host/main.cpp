@@ -11,7 +11,8 @@
 // Added: --seed N (the reference is unseeded), --device N, --bvh reference|sah, --sample-chunk N,
 // --dump-accum FILE (raw f64 [H][W][3] sums, row 0 = bottom), --side-len N (spheres),
 // --gpus N (devices [device, device + N): the frame's tiles sharded over N GPUs with an RCCL gather,
-// rt_render_multi — the counterpart of the reference's whole-machine rayon loop, main.rs:117-125).
+// rt_render_multi — the counterpart of the reference's whole-machine rayon loop, main.rs:117-125),
+// --partition tiles|samples (how --gpus splits the frame, RT_PARTITION_*; default: the library's).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -33,6 +34,7 @@ int verbose = 0;
 struct Args {
   std::string scene, output = "out.png", scene_output, scene_input, dump_accum, aspect = "std3x2", bvh = "reference";
   int samples = 100, max_reflect = 50, width = 640, device = 0, sample_chunk = 0, side_len = 11, gpus = 1;
+  int partition = RT_PARTITION_AUTO;
   double fov = 20.0, focal = 1.0, aperture = 0.001;
   bool night = false, single_threaded = false;
   unsigned long long seed = 0x5EED;
@@ -46,7 +48,8 @@ struct Args {
                "options: -o FILE -s N -m N -w N --single-threaded --camera-fov F --camera-focal-length F\n"
                "         --camera-aperture F --camera-aspect-ratio std3x2|std16x9|std16x10|square|target-iphone\n"
                "         --night --scene-output FILE (random)  <scene_input> (saved)  --side-len N (spheres)\n"
-               "         --seed N --device N --gpus N --bvh reference|sah --sample-chunk N --dump-accum FILE\n");
+               "         --seed N --device N --gpus N --partition tiles|samples --bvh reference|sah --sample-chunk N\n"
+               "         --dump-accum FILE\n");
   std::exit(2);
 }
 
@@ -77,6 +80,7 @@ int render_scene_multi(const Args& a, const rt_scene_desc* desc, const rt_camera
   p.seed = a.seed;
   p.tile_world = 1;
   p.sample_chunk = a.sample_chunk;
+  p.partition = a.partition;
   const size_t n = (size_t)cam.image_width * cam.image_height * 3;
   std::vector<double> accum(n);
   std::vector<uint8_t> rgb(n);
@@ -212,6 +216,12 @@ int main(int argc, char** argv) {
     else if (s == "--gpus") a.gpus = std::atoi(next().c_str());
     else if (s == "--bvh") a.bvh = next();
     else if (s == "--sample-chunk") a.sample_chunk = std::atoi(next().c_str());
+    else if (s == "--partition") {
+      const std::string v = next();
+      if (v == "tiles") a.partition = RT_PARTITION_TILES;
+      else if (v == "samples") a.partition = RT_PARTITION_SAMPLES;
+      else usage("--partition must be tiles or samples");
+    }
     else if (s == "--dump-accum") a.dump_accum = next();
     else if (s == "--side-len") a.side_len = std::atoi(next().c_str());
     else if (s == "-h" || s == "--help") usage("");

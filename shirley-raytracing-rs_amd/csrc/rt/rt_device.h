@@ -304,11 +304,28 @@ __device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Re
   return true;
 }
 
-// rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset
-template <int D1, int D2>
-__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out) {
+// rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset.
+// With `inv` (the ray's 1/d, each component the correctly rounded reciprocal: traverse4) the division
+// is Markstein's correction of a * (1/b) (div_recip), exactly the IEEE quotient for operands in
+// [2^-300, 2^300] (tools/divcheck.hip checks it on the GPU); other operands divide directly.
+#ifndef RT_RECT_INV_DIV
+#define RT_RECT_INV_DIV 0
+#endif
+template <int D1, int D2, bool INV = false>
+__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out,
+                                       v3 inv = V(0.0, 0.0, 0.0)) {
   constexpr int n = 3 - D1 - D2;
-  double t = (q[4] - comp(o, n)) / comp(d, n);
+  double t;
+  if constexpr (INV) {
+    const double num = q[4] - comp(o, n), den = comp(d, n);
+    const double an = fabs(num), ad = fabs(den);
+    if (an >= 0x1p-300 && an <= 0x1p300 && ad >= 0x1p-300 && ad <= 0x1p300)
+      t = div_recip(num, Recip{den, comp(inv, n)});
+    else
+      t = num / den;
+  } else {
+    t = (q[4] - comp(o, n)) / comp(d, n);
+  }
   if (t < t_min || t > t_max) return false;
   double d1v = comp(o, D1) + t * comp(d, D1);
   double d2v = comp(o, D2) + t * comp(d, D2);
@@ -319,28 +336,30 @@ __device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min
 
 // rect.rs:132-156 RectBox::hit — six faces in order, each against the running closest.
 // Returns the face index (0..5) that won, or -1.
-__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out) {
+template <bool INV = false>
+__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out,
+                                     v3 inv = V(0.0, 0.0, 0.0)) {
   double q[5];
   int face = -1;
   double tc = t_max, t;
   // xy_sides: (p0.x, p1.x, p0.y, p1.y, p1.z), (..., p0.z)
   q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
   q[4] = b[5];
-  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 0; }
+  if (rect_t<0, 1, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 0; }
   q[4] = b[2];
-  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 1; }
+  if (rect_t<0, 1, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 1; }
   // yz_sides: (p0.y, p1.y, p0.z, p1.z, p1.x), (..., p0.x)
   q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
   q[4] = b[3];
-  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 2; }
+  if (rect_t<1, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 2; }
   q[4] = b[0];
-  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 3; }
+  if (rect_t<1, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 3; }
   // xz_sides: (p0.x, p1.x, p0.z, p1.z, p1.y), (..., p0.y)
   q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
   q[4] = b[4];
-  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 4; }
+  if (rect_t<0, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 4; }
   q[4] = b[1];
-  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 5; }
+  if (rect_t<0, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 5; }
   t_out = tc;
   return face;
 }
@@ -974,6 +993,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
   // nodes in LDS: child k's word read back from the node (one address op and one ds_read) instead of
   // the select chain over c0..c3 (+0.3 %)
   constexpr bool kReread = (MODE == kNodesLds || MODE == kSceneLds) && !EXT;
+  constexpr bool kInvDiv = RT_RECT_INV_DIV != 0;  // rect / box faces divide through the ray's 1/d
   auto child = [&](int k) -> int { return kReread ? chp[k] : child_at(k, c0, c1, c2, c3); };
 #pragma unroll 1
   while (sph) {
@@ -1016,9 +1036,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     RT_STAT(++ptests);
     bool h;
     switch (pr.kind) {
-      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t); break;
-      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t); break;
-      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t);
+      case kPrimRectXY: h = rect_t<0, 1, kInvDiv>(pr.p, o, d, t_min, t_best, t, inv); break;
+      case kPrimRectYZ: h = rect_t<1, 2, kInvDiv>(pr.p, o, d, t_min, t_best, t, inv); break;
+      default: h = rect_t<0, 2, kInvDiv>(pr.p, o, d, t_min, t_best, t, inv);
     }
     if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
@@ -1039,7 +1059,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     }
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
     RT_STAT(++ptests);
-    const int f = box_t(pr.p, o, d, t_min, t_best, t);
+    const int f = box_t<kInvDiv>(pr.p, o, d, t_min, t_best, t, inv);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
   if (hit) tmaxf = tmax_f32(t_best);

@@ -15,7 +15,7 @@ import pytest
 
 import oracle_lib as O
 import raytracer as rt
-from test_gpu_parity import check_parity, EXACT_MIN
+from test_gpu_parity import check_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +42,7 @@ def test_range_matches_oracle_range(gpu, random_scene, engine):
     got = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=n, sample_begin=b, sample_count=n,
                                             engine=engine))
     want, ocnt = O.OracleScene(random_scene).render(cam, O.params(spp, 50, SEED, sample_begin=b, sample_count=n))
-    check_parity(got, want, n, frac_exact=EXACT_MIN["random"])
+    check_parity(got, want, n)  # (40 x 22 x 4 samples: the general 0.99 gate; only ulp-level marble sin differences)
     c = gpu.counters()
     assert c.samples == cam.image_width * cam.image_height * n == ocnt.samples
 

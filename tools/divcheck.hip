@@ -34,6 +34,10 @@ __global__ void check(uint64_t base, unsigned long long* bad) {
   const double q = a / b;
   const double f = div_recip(a, recip(b));
   if (__double_as_longlong(q) != __double_as_longlong(f)) atomicAdd(&bad[0], 1ull);
+  // Markstein's correction with the correctly rounded reciprocal 1.0 / b (the traversal's 1/d: rect and
+  // box faces divide through it, rt_device.h rect_t<.., INV>)
+  const double g = div_recip(a, Recip{b, 1.0 / b});
+  if (__double_as_longlong(q) != __double_as_longlong(g)) atomicAdd(&bad[3], 1ull);
   // unit vectors: component exponents within +-40 of a common one
   const int ec = (int)((h3 >> 32) % 521) - 260;
   const uint64_t g1 = mix(i * 5 + 11), g2 = mix(i * 5 + 12), g3 = mix(i * 5 + 13);
@@ -65,14 +69,15 @@ int main(int argc, char** argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 26;
   const int launches = argc > 2 ? atoi(argv[2]) : 16;
   unsigned long long* bad;
-  if (hipMalloc(&bad, 24) != hipSuccess) return 2;
-  (void)hipMemset(bad, 0, 24);
+  if (hipMalloc(&bad, 32) != hipSuccess) return 2;
+  (void)hipMemset(bad, 0, 32);
   const uint64_t per = 1ull << lg;
   for (int l = 0; l < launches; ++l)
     hipLaunchKernelGGL(check, dim3((unsigned)(per / 256)), dim3(256), 0, 0, (uint64_t)l * per, bad);
-  unsigned long long h[3];
-  if (hipMemcpy(h, bad, 24, hipMemcpyDeviceToHost) != hipSuccess) return 2;
-  printf("divcheck: %llu pairs, %llu division mismatches, %llu unit mismatches, %llu sqrt mismatches\n",
-         (unsigned long long)(per * launches), h[0], h[1], h[2]);
-  return (h[0] || h[1] || h[2]) ? 1 : 0;
+  unsigned long long h[4];
+  if (hipMemcpy(h, bad, 32, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+  printf("divcheck: %llu pairs, %llu division mismatches, %llu unit mismatches, %llu sqrt mismatches, "
+         "%llu inverse-division mismatches\n",
+         (unsigned long long)(per * launches), h[0], h[1], h[2], h[3]);
+  return (h[0] || h[1] || h[2] || h[3]) ? 1 : 0;
 }
