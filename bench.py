@@ -314,7 +314,10 @@ def main():
                                  sample_chunk=args.sample_chunk, tile_rank=rank, tile_world=world,
                                  engine=args.engine, timing=args.timing, partition=args.partition,
                                  scratch_mb=args.scratch_mb)
-    stream = torch.cuda.current_stream()
+    # a stream of our own: the render calls, the HIP events and the host copy share it (torch's default
+    # stream has handle 0, which the C ABI reads as "the ctx's own stream")
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sh = stream.cuda_stream
     accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     comm = None

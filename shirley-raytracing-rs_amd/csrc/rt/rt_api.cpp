@@ -849,7 +849,12 @@ int resolve_range(rt_ctx* c, const rt_render_params* p, SampleRange* r) {
   return RT_OK;
 }
 
-constexpr long long kDefaultScratchMiB = 512;
+// Default bound of a call's partial sums.  A sample pass costs a fixed ~2.6 ms on MI355X (its launch's
+// ramp and drain, measured: the headline frame in 3 passes of <= 512 MiB ran 189.5 ms of trace against
+// 181.7 ms in one pass), so passes are sized large: 2 GiB keeps the headline (1.45 GB) and every
+// per-rank frame of the multi-GPU partitions in one pass and cuts the 1920x1080 @ 2000-spp frames'
+// 6.2 GB into 4 passes (+0.3 %).  scratch_mb sets any other bound (down to one chunk per pass).
+constexpr long long kDefaultScratchMiB = 2048;
 
 // trace + reduce of samples [R.begin, R.end) for tile rows [ty0, ty1); out layout: packed tiles
 // (packed=1) or rows [row0, row1).  The call's work units (pixel x chunk of samples) are traced in
@@ -1130,10 +1135,6 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     // a sphere's 1 / radius (sphere.rs:48 `scale(1.0 / self.radius)`), the same IEEE quotient the device
     // would compute per hit record; p[4] is otherwise unused by spheres
     if (q.kind == kPrimSphere || q.kind == kPrimMovingSphere) q.p[4] = 1.0 / q.p[3];
-    // a sphere's inner radius for the box test's fast accept (rt_device.h leaf_tests4): r - 2 m, m =
-    // 2^-46 (B + L) with B the largest box plane and L the origin bound of the f32 node test (the
-    // rounding of this subtraction, <= 2^-53 r, stays far inside the second m)
-    if (q.kind == kPrimSphere) q.p[5] = q.p[3] - 2.0 * std::ldexp(infl.box_bound + (double)infl.origin_limit, -46);
     q.material = o.material | (d->materials[o.material].kind == RT_MAT_DIELECTRIC ? kPrimMatDielectric : 0);
     if (is_extended(o)) {
       if (exts.size() >= (1u << (31 - kPrimExtShift)))

@@ -203,11 +203,6 @@ __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t
 // ------------------------------------------------------------------------------------------
 // intersection (t only during traversal; the full hit record is rebuilt for the winner)
 // ------------------------------------------------------------------------------------------
-// (A/B switch) node visits derive the hit-leaf mask from the box compares themselves (RT_VISIT_HC = 1)
-// instead of re-testing the keys' bits
-#ifndef RT_VISIT_HC
-#define RT_VISIT_HC 0
-#endif
 // ------------------------------------------------------------------------------------------
 // aabb.rs:62-79 hit2, per axis: t0 = (min - o) * inv, t1 = (max - o) * inv, swapped when inv < 0,
 // t_min = t0 > t_min ? t0 : t_min, t_max = t1 < t_max ? t1 : t_max, miss when t_max <= t_min
@@ -288,8 +283,8 @@ __device__ __forceinline__ double div_by(double n, const Recip& R, bool ok) {
   return n / R.b;
 }
 __device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Recip& ra, bool ra_ok, double t_min,
-                                           double t_max, double& t, v3& oc) {
-  oc = o - V(p[0], p[1], p[2]);
+                                           double t_max, double& t) {
+  v3 oc = o - V(p[0], p[1], p[2]);
   double half_b = dot(oc, d);
   double c = len2(oc) - p[3] * p[3];
   double disc = half_b * half_b - ra.b * c;
@@ -304,28 +299,11 @@ __device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Re
   return true;
 }
 
-// rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset.
-// With `inv` (the ray's 1/d, each component the correctly rounded reciprocal: traverse4) the division
-// is Markstein's correction of a * (1/b) (div_recip), exactly the IEEE quotient for operands in
-// [2^-300, 2^300] (tools/divcheck.hip checks it on the GPU); other operands divide directly.
-#ifndef RT_RECT_INV_DIV
-#define RT_RECT_INV_DIV 0
-#endif
-template <int D1, int D2, bool INV = false>
-__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out,
-                                       v3 inv = V(0.0, 0.0, 0.0)) {
+// rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset
+template <int D1, int D2>
+__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out) {
   constexpr int n = 3 - D1 - D2;
-  double t;
-  if constexpr (INV) {
-    const double num = q[4] - comp(o, n), den = comp(d, n);
-    const double an = fabs(num), ad = fabs(den);
-    if (an >= 0x1p-300 && an <= 0x1p300 && ad >= 0x1p-300 && ad <= 0x1p300)
-      t = div_recip(num, Recip{den, comp(inv, n)});
-    else
-      t = num / den;
-  } else {
-    t = (q[4] - comp(o, n)) / comp(d, n);
-  }
+  double t = (q[4] - comp(o, n)) / comp(d, n);
   if (t < t_min || t > t_max) return false;
   double d1v = comp(o, D1) + t * comp(d, D1);
   double d2v = comp(o, D2) + t * comp(d, D2);
@@ -336,30 +314,28 @@ __device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min
 
 // rect.rs:132-156 RectBox::hit — six faces in order, each against the running closest.
 // Returns the face index (0..5) that won, or -1.
-template <bool INV = false>
-__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out,
-                                     v3 inv = V(0.0, 0.0, 0.0)) {
+__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out) {
   double q[5];
   int face = -1;
   double tc = t_max, t;
   // xy_sides: (p0.x, p1.x, p0.y, p1.y, p1.z), (..., p0.z)
   q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
   q[4] = b[5];
-  if (rect_t<0, 1, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 0; }
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 0; }
   q[4] = b[2];
-  if (rect_t<0, 1, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 1; }
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 1; }
   // yz_sides: (p0.y, p1.y, p0.z, p1.z, p1.x), (..., p0.x)
   q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
   q[4] = b[3];
-  if (rect_t<1, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 2; }
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 2; }
   q[4] = b[0];
-  if (rect_t<1, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 3; }
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 3; }
   // xz_sides: (p0.x, p1.x, p0.z, p1.z, p1.y), (..., p0.y)
   q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
   q[4] = b[4];
-  if (rect_t<0, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 4; }
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 4; }
   q[4] = b[1];
-  if (rect_t<0, 2, INV>(q, o, d, t_min, tc, t, inv)) { tc = t; face = 5; }
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 5; }
   t_out = tc;
   return face;
 }
@@ -893,7 +869,7 @@ __device__ __forceinline__ void node4_keys(const N4& nd, const RayF& r, v3 o, v3
     for (int e = 0; e < 2; ++e) {
       const float tn = fmaxf(fmaxf(x0[e], y0[e]), fmaxf(z0[e], tminf));
       const float tf = fminf(fminf(x1[e], y1[e]), fminf(z1[e], tmaxf));
-      hc[2 * h + e] = tn <= tf ? chw[2 * h + e] : 0u;  // the child word where its box is hit (RT_VISIT_HC)
+      hc[2 * h + e] = tn <= tf ? chw[2 * h + e] : 0u;  // the child word where its box is hit
       key[2 * h + e] = tn <= tf ? tn : (M1 ? __uint_as_float(~0u) : __builtin_inff());
     }
   }
@@ -975,13 +951,9 @@ __device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned
   return __builtin_amdgcn_perm(w1, w0, 0x0c0c0703u) | __builtin_amdgcn_perm(w3, w2, 0x07030c0cu);
 }
 
-// (A/B switch) a sphere hit skips the exact test of its bounding box where that test provably passes
-#ifndef RT_SPHERE_FAST_ACCEPT
-#define RT_SPHERE_FAST_ACCEPT 0
-#endif
 template <int MODE, bool EXT>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
-                                            RaySigns ns, bool fast, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
+                                            RaySigns ns, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, const int32_t* chp, double& t_best, float& tmaxf, int& best,
                                             int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
   // lm: spread mask of hit leaf children (bit 8 i + 7: child i).  A leaf's child word is
@@ -993,7 +965,6 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
   // nodes in LDS: child k's word read back from the node (one address op and one ds_read) instead of
   // the select chain over c0..c3 (+0.3 %)
   constexpr bool kReread = (MODE == kNodesLds || MODE == kSceneLds) && !EXT;
-  constexpr bool kInvDiv = RT_RECT_INV_DIV != 0;  // rect / box faces divide through the ray's 1/d
   auto child = [&](int k) -> int { return kReread ? chp[k] : child_at(k, c0, c1, c2, c3); };
 #pragma unroll 1
   while (sph) {
@@ -1008,19 +979,8 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double t;
     PH_COUNT(3);
     RT_STAT(++ptests);
-    v3 oc;
-    if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t, oc)) continue;
-#if RT_SPHERE_FAST_ACCEPT
-    // The box test passes for sure when the hit point o + t d lies strictly inside the sphere's box by
-    // the scene's margin on every axis and t_min < t < t_best (then every FP slab entry
-    // is < t and every exit > t); p[5] = r - margin (host, <= 0 for a negative radius: never sure).  The
-    // check only decides whether the exact test runs; a lane it does not clear runs slab_sphere.
-    const bool sure = fast && t > t_min && t < t_best && fabs(fma(t, d.x, oc.x)) < pr.p[5] &&
-                      fabs(fma(t, d.y, oc.y)) < pr.p[5] && fabs(fma(t, d.z, oc.z)) < pr.p[5];
-    if (!sure && !slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
-#elif !defined(RT_EXP_NO_SPHERE_BOX)  // (timing experiment only: drops the reference's box test)
+    if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) continue;
     if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
-#endif
     t_best = t; best = leaf; face_best = -1; hit = true;
   }
 #pragma unroll 1
@@ -1036,9 +996,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     RT_STAT(++ptests);
     bool h;
     switch (pr.kind) {
-      case kPrimRectXY: h = rect_t<0, 1, kInvDiv>(pr.p, o, d, t_min, t_best, t, inv); break;
-      case kPrimRectYZ: h = rect_t<1, 2, kInvDiv>(pr.p, o, d, t_min, t_best, t, inv); break;
-      default: h = rect_t<0, 2, kInvDiv>(pr.p, o, d, t_min, t_best, t, inv);
+      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t); break;
+      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t); break;
+      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t);
     }
     if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
@@ -1059,7 +1019,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     }
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
     RT_STAT(++ptests);
-    const int f = box_t<kInvDiv>(pr.p, o, d, t_min, t_best, t, inv);
+    const int f = box_t(pr.p, o, d, t_min, t_best, t);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
   if (hit) tmaxf = tmax_f32(t_best);
@@ -1096,24 +1056,14 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const N4* lds_n
   unsigned hc[4];
   node4_keys<kM1>(nd, rf, o, inv, tminf, tmaxf, t_min, t_best, k0, k1, k2, k3, ch, hc);
   RT_STAT(visits += 4);
-#if RT_VISIT_HC
   // hit leaf: the child word where the box test passed (the key's own compare, no second test), else 0;
-  // its sign bit marks a leaf, gathered into the spread mask
+  // its sign bit marks a leaf, gathered into the spread mask (4 VALU per visit fewer than re-testing the
+  // keys' bits)
   return top_bytes(hc[0], hc[1], hc[2], hc[3]) & 0x80808080u;
-#endif
   // hit leaf: key < inf (bits(k) + 0x80800000 keeps the sign bit exactly for bits(k) < bits(inf); keys
   // are >= 0) and a negative child word; as a spread mask
   // (an M1 miss key ~0u: its sum keeps the top bit, so it is masked by ~bits(k) — one v_bitop3 with the
   // child)
-#if !RT_VISIT_HC
-  const unsigned m0 = kM1 ? ~__float_as_uint(k0) : ~0u, m1 = kM1 ? ~__float_as_uint(k1) : ~0u;
-  const unsigned m2 = kM1 ? ~__float_as_uint(k2) : ~0u, m3 = kM1 ? ~__float_as_uint(k3) : ~0u;
-  const unsigned h0 = (__float_as_uint(k0) + 0x80800000u) & m0 & (unsigned)ch.x;
-  const unsigned h1 = (__float_as_uint(k1) + 0x80800000u) & m1 & (unsigned)ch.y;
-  const unsigned h2 = (__float_as_uint(k2) + 0x80800000u) & m2 & (unsigned)ch.z;
-  const unsigned h3 = (__float_as_uint(k3) + 0x80800000u) & m3 & (unsigned)ch.w;
-  return top_bytes(h0, h1, h2, h3) & 0x80808080u;
-#endif
 }
 // visit4's ordering part: internal children as packed words (a miss, k = inf or ~0u, packs above any
 // bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.
@@ -1162,7 +1112,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<E
                                         visits, chp);
   if (lm) PH_COUNT(1);
   if (lm)
-    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, rf.fast, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
+    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
                            face_best, rk, seed, ptests);
   return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
 }
