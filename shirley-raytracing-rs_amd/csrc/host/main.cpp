@@ -12,7 +12,10 @@
 // --dump-accum FILE (raw f64 [H][W][3] sums, row 0 = bottom), --side-len N (spheres),
 // --gpus N (devices [device, device + N): the frame's tiles sharded over N GPUs with an RCCL gather,
 // rt_render_multi — the counterpart of the reference's whole-machine rayon loop, main.rs:117-125),
-// --partition tiles|samples (how --gpus splits the frame, RT_PARTITION_*; default: the library's).
+// --partition tiles|samples (how --gpus splits the frame, RT_PARTITION_*; default: the library's),
+// --progressive K (the frame's samples in K consecutive ranges, rt_render_params.sample_begin / count;
+// after each range the running sums go to --dump-accum FILE + FILE.json and the PNG shows the samples so
+// far: a checkpoint), --resume FILE (continue from such a checkpoint: its sums cover samples [0, N)).
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -35,6 +38,8 @@ struct Args {
   std::string scene, output = "out.png", scene_output, scene_input, dump_accum, aspect = "std3x2", bvh = "reference";
   int samples = 100, max_reflect = 50, width = 640, device = 0, sample_chunk = 0, side_len = 11, gpus = 1;
   int partition = RT_PARTITION_AUTO;
+  int progressive = 1;
+  std::string resume;
   double fov = 20.0, focal = 1.0, aperture = 0.001;
   bool night = false, single_threaded = false;
   unsigned long long seed = 0x5EED;
@@ -49,7 +54,7 @@ struct Args {
                "         --camera-aperture F --camera-aspect-ratio std3x2|std16x9|std16x10|square|target-iphone\n"
                "         --night --scene-output FILE (random)  <scene_input> (saved)  --side-len N (spheres)\n"
                "         --seed N --device N --gpus N --partition tiles|samples --bvh reference|sah --sample-chunk N\n"
-               "         --dump-accum FILE\n");
+               "         --dump-accum FILE --progressive K --resume FILE\n");
   std::exit(2);
 }
 
@@ -137,7 +142,69 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
   std::vector<double> accum;
   std::vector<uint8_t> rgb(n);
   auto t1 = std::chrono::steady_clock::now();
-  if (!a.dump_accum.empty()) {  // the raw sums are wanted on the host: render + host tonemap
+  if (a.progressive > 1 || !a.resume.empty()) {
+    // progressive rendering with checkpoints: sample ranges [b_k, b_k+1) of the frame; the host adds each
+    // range's sums to the running sums in range order (so a resumed run adds exactly what an
+    // uninterrupted one does) and writes the checkpoint after every range
+    accum.assign(n, 0.0);
+    int done = 0;
+    if (!a.resume.empty()) {
+      std::ifstream fj(a.resume + ".json");
+      std::string js((std::istreambuf_iterator<char>(fj)), std::istreambuf_iterator<char>());
+      const size_t k = js.find("\"samples_done\":");
+      std::ifstream f(a.resume, std::ios::binary);
+      f.read((char*)accum.data(), (std::streamsize)(n * sizeof(double)));
+      if (k == std::string::npos || !f || f.gcount() != (std::streamsize)(n * sizeof(double))) {
+        std::fprintf(stderr, "error: %s is not a checkpoint of this frame\n", a.resume.c_str());
+        rt_destroy(ctx);
+        return 1;
+      }
+      done = std::atoi(js.c_str() + k + 15);
+      if (done < 0 || done > samples) {
+        std::fprintf(stderr, "error: checkpoint covers %d samples of %d\n", done, samples);
+        rt_destroy(ctx);
+        return 1;
+      }
+    }
+    std::vector<double> part(n);
+    const int ranges = std::max(1, a.progressive);
+    const int left = samples - done;
+    for (int k = 0; k < ranges && left > 0; ++k) {
+      const int b = done + (int)((long long)left * k / ranges), e = done + (int)((long long)left * (k + 1) / ranges);
+      if (e <= b) continue;
+      p.sample_begin = b;
+      p.sample_count = e - b;
+      if ((st = rt_render(ctx, &cam, &p, part.data()))) {
+        std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
+        rt_destroy(ctx);
+        return 1;
+      }
+      for (size_t i = 0; i < n; ++i) accum[i] += part[i];
+      rt_tonemap(accum.data(), cam.image_width, cam.image_height, e, rgb.data());
+      if (!a.dump_accum.empty()) {
+        std::ofstream f(a.dump_accum, std::ios::binary);
+        f.write((const char*)accum.data(), (std::streamsize)(n * sizeof(double)));
+        std::ofstream fj(a.dump_accum + ".json");
+        fj << "{\"samples_done\": " << e << ", \"samples\": " << samples << ", \"width\": " << cam.image_width
+           << ", \"height\": " << cam.image_height << ", \"seed\": " << a.seed << "}\n";
+      }
+      if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
+        std::fprintf(stderr, "error: %s\n", sh_last_error());
+        rt_destroy(ctx);
+        return 1;
+      }
+      if (verbose >= 1) std::fprintf(stderr, "INFO checkpoint: samples [0, %d) of %d\n", e, samples);
+    }
+    rt_destroy(ctx);
+    if (left == 0) {  // a complete checkpoint: just its picture
+      rt_tonemap(accum.data(), cam.image_width, cam.image_height, samples, rgb.data());
+      if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
+        std::fprintf(stderr, "error: %s\n", sh_last_error());
+        return 1;
+      }
+    }
+    return 0;
+  } else if (!a.dump_accum.empty()) {  // the raw sums are wanted on the host: render + host tonemap
     accum.resize(n);
     if ((st = rt_render(ctx, &cam, &p, accum.data()))) {
       std::fprintf(stderr, "error: %s\n", rt_last_error(ctx));
@@ -216,6 +283,8 @@ int main(int argc, char** argv) {
     else if (s == "--gpus") a.gpus = std::atoi(next().c_str());
     else if (s == "--bvh") a.bvh = next();
     else if (s == "--sample-chunk") a.sample_chunk = std::atoi(next().c_str());
+    else if (s == "--progressive") a.progressive = std::atoi(next().c_str());
+    else if (s == "--resume") a.resume = next();
     else if (s == "--partition") {
       const std::string v = next();
       if (v == "tiles") a.partition = RT_PARTITION_TILES;
@@ -237,6 +306,8 @@ int main(int argc, char** argv) {
   a.scene = pos[1];
   if (a.samples < 0 || a.max_reflect < 0 || a.width < 1) usage("samples / max-reflect / width out of range");
   if (a.gpus < 1 || a.gpus > 64) usage("--gpus must be in [1, 64]");
+  if (a.progressive < 1) usage("--progressive must be >= 1");
+  if (a.gpus > 1 && (a.progressive > 1 || !a.resume.empty())) usage("--progressive / --resume render on one GPU");
 
   sh_scene* scene = nullptr;
   std::string cam_scene = a.scene;

@@ -11,6 +11,13 @@ import torch.multiprocessing as mp
 W, H, SPP, SEED = 27, 19, 2, 0x5EED  # partial tiles on both axes
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _frame_pixels(py, px):
     import oracle_lib as O
     import raytracer as rt
@@ -54,8 +61,7 @@ def _worker(rank, world, port, result_path):
 
 @pytest.mark.parametrize("world", [2, 5])  # 12 tiles: even, and uneven with padded ranks
 def test_two_rank_tile_gather_equals_single_frame(tmp_path, world):
-    import random
-    port = 29500 + random.randint(0, 2000)
+    port = _free_port()
     out = str(tmp_path / "img.npy")
     mp.spawn(_worker, args=(world, port, out), nprocs=world, join=True)
     img = np.load(out)
@@ -110,9 +116,8 @@ def test_sample_split_reduce_equals_rank_order_sum(tmp_path, world):
     row bands are exchanged (all-to-all), summed in rank order and gathered to rank 0.  The result equals
     the rank-order sum of the shares bit for bit, and the one-range frame within reassociation
     (|d| <= 1e-12 |sum|)."""
-    import random
     from raytracer import parallel as P
-    port = 29500 + random.randint(0, 2000)
+    port = _free_port()
     out = str(tmp_path / "img.npy")
     mp.spawn(_sample_worker, args=(world, port, out), nprocs=world, join=True)
     img = np.load(out)

@@ -153,3 +153,35 @@ def test_scene_digest_on_device(gpu, random_scene):
     assert gpu.digest() == d
     gpu.upload(rt.scenes.create_cornell_box().finalize(SEED), "sah")
     assert gpu.digest() != d
+
+
+def test_cli_progressive_checkpoints_and_resume(tmp_path):
+    """ray-cli --progressive K renders the frame as K sample ranges and checkpoints the running sums after
+    each (--dump-accum FILE + FILE.json); --resume continues a checkpoint.  The resumed run ends with the
+    same bits as the uninterrupted one (the same ranges added in the same order), and both equal the
+    one-call frame within reassociation."""
+    import json
+    import os
+    import subprocess
+    from raytracer import _native as N
+    cli = os.path.join(N.BIN_DIR, "ray-cli")
+    common = ["render", "random", "-w", "48", "-s", "12", "--seed", "0x5EED", "--sample-chunk", "2"]
+    one, full, part = (str(tmp_path / n) for n in ("one.bin", "full.bin", "part.bin"))
+    for extra in (["--dump-accum", one],
+                  ["--progressive", "3", "--dump-accum", full]):
+        r = subprocess.run([cli] + common + ["-o", str(tmp_path / "x.png")] + extra, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+    assert json.load(open(full + ".json"))["samples_done"] == 12
+    # interrupted after the first of 3 ranges (samples [0, 4)), then resumed for the rest
+    r = subprocess.run([cli] + ["render", "random", "-w", "48", "-s", "4", "--seed", "0x5EED", "--sample-chunk", "2",
+                                "-o", str(tmp_path / "y.png"), "--progressive", "1", "--dump-accum", part],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert json.load(open(part + ".json"))["samples_done"] == 4
+    r = subprocess.run([cli] + common + ["-o", str(tmp_path / "z.png"), "--progressive", "2", "--resume", part,
+                                         "--dump-accum", part], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    a = np.fromfile(full)
+    assert np.array_equal(np.fromfile(part), a)
+    b = np.fromfile(one)
+    assert np.all(np.abs(a - b) <= REASSOC * np.abs(b) + 1e-300)
