@@ -243,9 +243,12 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
                  std::chrono::duration<double, std::milli>(t1 - t0).count(), ms, cnt.kernel_ms, cnt.reduce_ms, msamp,
                  (double)cnt.segments / (double)(cnt.samples ? cnt.samples : 1));
   rt_destroy(ctx);
-  if (!a.dump_accum.empty()) {
+  if (!a.dump_accum.empty()) {  // a complete checkpoint (--resume reads FILE.json's samples_done)
     std::ofstream f(a.dump_accum, std::ios::binary);
     f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
+    std::ofstream fj(a.dump_accum + ".json");
+    fj << "{\"samples_done\": " << samples << ", \"samples\": " << samples << ", \"width\": " << cam.image_width
+       << ", \"height\": " << cam.image_height << ", \"seed\": " << a.seed << "}\n";
   }
   if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
     std::fprintf(stderr, "error: %s\n", sh_last_error());

@@ -949,18 +949,12 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
   kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
 
   const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
-  // segment counters, then the shared tail counter in its own 64-B line (DWork.seg_units)
-  const size_t counter_bytes = ((size_t)nseg * sizeof(uint32_t) + 63) / 64 * 64 + 64;
   {
-    st = ensure(c, c->unit_counter, counter_bytes);
+    const size_t bytes = std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t));
+    st = ensure(c, c->unit_counter, bytes);
     if (st) return st;
     kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
   }
-  // the tail: the rank's last tiles in tile-major order (the top rows of the picture) — for the
-  // headline frame its sky — handed out after the segments (trace.hip); SHIRLEY_TAIL_FRAC: tuning
-  double tail_frac = 1.0 / 16.0;
-  if (const char* e = getenv("SHIRLEY_TAIL_FRAC")) tail_frac = std::max(0.0, std::min(1.0, atof(e)));
-  const long long tail_tiles = std::min<long long>(L.n_tiles_rank, (long long)std::ceil(tail_frac * L.n_tiles_rank));
   if ((int)c->pass_ev.size() < 2 * passes) {
     const size_t have = c->pass_ev.size();
     c->pass_ev.resize(2 * passes, nullptr);
@@ -1011,16 +1005,15 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     // for units of >= 4 samples (measured, session T: headline +2 %, gen_spheres +11 %, final_scene
     // +2.4 %, 2 ranks +2.4 %; with 1- or 2-sample units — small frames, 4 and 8 ranks — the shared
     // queue is as fast or faster: cfg1 -17 %, the 8-rank frame -6 % with segments)
+    const uint64_t per = (w.n_units + nseg - 1) / nseg;
     w.n_segs = (engine == RT_ENGINE_MEGAKERNEL && chunk >= 4) ? (uint32_t)nseg : 0u;
-    w.seg_units = (uint64_t)(L.n_tiles_rank - tail_tiles) * (uint64_t)w.n_chunks * (uint64_t)kTilePixels;
-    const uint64_t seg_per = (w.seg_units + nseg - 1) / nseg;
-    w.seg_len = (uint32_t)std::max<uint64_t>(kWave, (seg_per + kWave - 1) / kWave * kWave);
+    w.seg_len = (uint32_t)std::max<uint64_t>(kWave, (per + kWave - 1) / kWave * kWave);
     // the device copy is taken after every field is set (the kernel may read any of them)
     c->host_work[k] = w;
     void* kwork = static_cast<char*>(c->kcam.p) + 2 * sizeof(DCamera) + (size_t)k * sizeof(DWork);  // (16-B aligned)
     HIP_TRY(c, hipMemcpyAsync(kwork, &c->host_work[k], sizeof(DWork), hipMemcpyHostToDevice, s));
     kp.work_const = (uint64_t)(uintptr_t)kwork;
-    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, counter_bytes, s));
+    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t)), s));
     HIP_TRY(c, hipEventRecord(c->pass_ev[2 * k], s));
     if (engine == RT_ENGINE_WAVEFRONT) {
       st = run_wavefront(c, kp, timing, s);

@@ -209,11 +209,6 @@ struct DWork {
   // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
   // segment, then steal from the next segments that still hold units
   uint32_t seg_len, n_segs;
-  // units [0, seg_units) are cut into the segments; the rest — the last tile rows of the window, the top
-  // of the picture — are handed out from one shared 64-bit counter once every segment is empty, so a
-  // frame ends on those rows' units (the sky: short paths, a short tail).  The counter sits in its own
-  // 64-B line after the segment counters: byte offset round_up(4 n_segs, 64) of KParams.unit_counter.
-  uint64_t seg_units;
 };
 
 // Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot

@@ -217,7 +217,7 @@ void trace_kernel(KParams P) {
           unsigned off = 0;
           if (lane == 0) off = atomicAdd(ctr + seg, (unsigned)kWave);
           off = (unsigned)__builtin_amdgcn_readfirstlane((int)off);
-          if (off < W.seg_len && (unsigned long long)seg * W.seg_len + off < W.seg_units) {
+          if (off < W.seg_len && (unsigned long long)seg * W.seg_len + off < W.n_units) {
             nb = (unsigned long long)seg * W.seg_len + off;
             break;
           }
@@ -228,7 +228,7 @@ void trace_kernel(KParams P) {
             bool has = false;
             if (base + (uint32_t)lane < W.n_segs) {
               const unsigned o = __hip_atomic_load(ctr + cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              has = o < W.seg_len && (unsigned long long)cand * W.seg_len + o < W.seg_units;
+              has = o < W.seg_len && (unsigned long long)cand * W.seg_len + o < W.n_units;
             }
             const unsigned long long m = __ballot(has);
             if (m != 0ull) {
@@ -237,17 +237,7 @@ void trace_kernel(KParams P) {
               break;
             }
           }
-          if (!found) {
-            // every segment is empty: the shared tail (the last rows' units), then the end
-            unsigned long long t = 0;
-            if (lane == 0)
-              t = atomicAdd(reinterpret_cast<unsigned long long*>(ctr) + ((W.n_segs + 15u) / 16u) * 8u,
-                            (unsigned long long)kWave);
-            t = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(t >> 32)) << 32) |
-                (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)t);
-            nb = W.seg_units + t;
-            break;
-          }
+          if (!found) break;
         }
         } else {  // one shared queue (short units: DWork.n_segs = 0)
           nb = 0;
