@@ -14,6 +14,7 @@
 #   prof[:bench.py args]     rocprofv3 --kernel-trace --stats (kernel_stats.csv under <tag>/prof)
 #   pmc:<COUNTERS>[:args]    one rocprofv3 --pmc pass (counters comma-separated, one block's limits)
 #   py:<script> [args]       a python tool (e.g. "py:tools/shard_balance.py gpurun_out/x/shard.json")
+#   sh:<command line>        any command, run by bash -c as written
 # Recipes (profiles/<round>/ evidence):
 #   kernel stats + HBM traffic:  prof pmc:FETCH_SIZE pmc:WRITE_SIZE, then
 #                                python tools/pmc_traffic.py gpurun_out/<tag> profiles/<round> "<workload>" sah
@@ -98,6 +99,9 @@ for step in "$@"; do
         python3 bench.py ${pargs:---steps 1 --warmup 0 --no-cpu --no-configs} > "$log" 2>&1
       rc=$?; echo "[$n pmc $counters] rc=$rc"
       find "$d" -name "*counter_collection.csv" | head -2 ;;
+    sh)  # sh:<command line> — run as written by bash (quoting kept)
+      timeout -k 10 600 bash -c "$args" > "$log" 2>&1
+      rc=$?; echo "[$n sh $args] rc=$rc"; tail -30 "$log" ;;
     py)
       timeout -k 10 900 python -u $args > "$log" 2>&1
       rc=$?; echo "[$n py $args] rc=$rc"; tail -3 "$log" ;;
