@@ -203,6 +203,9 @@ __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t
 // ------------------------------------------------------------------------------------------
 // intersection (t only during traversal; the full hit record is rebuilt for the winner)
 // ------------------------------------------------------------------------------------------
+#ifndef RT_POP_SKIP
+#define RT_POP_SKIP 0
+#endif
 // ------------------------------------------------------------------------------------------
 // aabb.rs:62-79 hit2, per axis: t0 = (min - o) * inv, t1 = (max - o) * inv, swapped when inv < 0,
 // t_min = t0 > t_min ? t0 : t_min, t_max = t1 < t_max ? t1 : t_max, miss when t_max <= t_min
@@ -1090,6 +1093,24 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   if (p2 <= lim) { stk[sp] = top; sp += STRIDE; top = p2; }
   if (p1 <= lim) { stk[sp] = top; sp += STRIDE; top = p1; }
   if (p0 <= lim) return (int)(p0 & km);
+#if RT_POP_SKIP
+  // (A/B switch) culled entries are skipped in a loop with a single-compare exit (lim < e < ~0u as one
+  // unsigned range test); the accepted entry is then popped once
+  const unsigned lo = lim + 1u, span = ~0u - lo;
+  unsigned e = top;
+  while (e - lo < span) {
+    PH_COUNT(5);
+    sp -= STRIDE;
+    e = stk[sp];
+  }
+  if (e == ~0u) {
+    top = e;
+    return -1;
+  }
+  sp -= STRIDE;  // e is a real entry: the ~0u sentinel lies below it
+  top = stk[sp];
+  return (int)(e & km);
+#else
   for (;;) {
     PH_COUNT(5);
     const unsigned e = top;
@@ -1098,6 +1119,7 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
     top = stk[sp];
     if (e <= lim) return (int)(e & km);
   }
+#endif
 }
 template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
