@@ -214,6 +214,11 @@ static hit_t make_hit(const ray_t* in, v3 point, v3 normal, double t, double u, 
 
 static const double PI_ = 3.14159265358979323846;
 
+/* statistics hook (tools/sphere_stats.c): outcome k = 0 miss (disc < 0), 1 no root in range, 2 hit */
+#ifndef OR_SPHERE_STAT
+#define OR_SPHERE_STAT(k, oc, d, half_b, cc, radius, disc)
+#endif
+
 /* sphere.rs:28-52 (+ get_uv 17-26) */
 static int sphere_hit(const double* p, const ray_t* r, double t_min, double t_max, hit_t* out) {
   v3 c = V(p[0], p[1], p[2]);
@@ -223,13 +228,20 @@ static int sphere_hit(const double* p, const ray_t* r, double t_min, double t_ma
   double half_b = vdot(oc, r->d);
   double cc = vlen2(oc) - radius * radius;
   double disc = half_b * half_b - a * cc;
-  if (disc < 0.0) return 0;
+  if (disc < 0.0) {
+    OR_SPHERE_STAT(0, oc, r->d, half_b, cc, radius, disc);
+    return 0;
+  }
   double sqrt_d = sqrt(disc);
   double root = (-half_b - sqrt_d) / a;
   if (root < t_min || t_max < root) {
     root = (-half_b + sqrt_d) / a;
-    if (root < t_min || t_max < root) return 0;
+    if (root < t_min || t_max < root) {
+      OR_SPHERE_STAT(1, oc, r->d, half_b, cc, radius, disc);
+      return 0;
+    }
   }
+  OR_SPHERE_STAT(2, oc, r->d, half_b, cc, radius, disc);
   v3 point = ray_at(r, root);
   v3 normal = vscale(vsub(point, c), 1.0 / radius);
   double theta = acos(-normal.y);
