@@ -192,7 +192,7 @@ typedef struct rt_render_params {
   /* multi-GPU entry points (rt_render_sharded / rt_render_multi): how the frame is split over the ranks,
    * RT_PARTITION_*; ignored by the single-device calls */
   int32_t partition;
-  /* bound on the per-call partial-sum scratch in MiB (0 = default 2048).  A call whose [chunks][pixels][3]
+  /* bound on the per-call partial-sum scratch in MiB (0 = default 8192).  A call whose [chunks][pixels][3]
    * f64 partial sums exceed it renders its chunks in consecutive sample passes, each reduced into the
    * output in chunk order — the same per-pixel additions in the same order as one pass, so the frame is
    * bit-identical for every bound. */

@@ -16,6 +16,7 @@
 
 #include "../../../include/shirley_rt.h"
 #include "bvh_build.h"
+#include "plan.h"
 #include "rccl_loader.h"
 #include "rt_layout.h"
 
@@ -662,7 +663,6 @@ int check_render_args(rt_ctx* c, const rt_camera* cam, const rt_render_params* p
   return RT_OK;
 }
 
-constexpr int kWfDefaultChunk = 8;
 constexpr long long kWfDefaultSlots = 1LL << 21;
 constexpr int kWfBatch = 32;  // iterations launched between two host checks of the termination flag
 
@@ -849,13 +849,6 @@ int resolve_range(rt_ctx* c, const rt_render_params* p, SampleRange* r) {
   return RT_OK;
 }
 
-// Default bound of a call's partial sums.  A sample pass costs a fixed ~2.6 ms on MI355X (its launch's
-// ramp and drain, measured: the headline frame in 3 passes of <= 512 MiB ran 189.5 ms of trace against
-// 181.7 ms in one pass), so passes are sized large: 2 GiB keeps the headline (1.45 GB) and every
-// per-rank frame of the multi-GPU partitions in one pass and cuts the 1920x1080 @ 2000-spp frames'
-// 6.2 GB into 4 passes (+0.3 %).  scratch_mb sets any other bound (down to one chunk per pass).
-constexpr long long kDefaultScratchMiB = 2048;
-
 // trace + reduce of samples [R.begin, R.end) for tile rows [ty0, ty1); out layout: packed tiles
 // (packed=1) or rows [row0, row1).  The call's work units (pixel x chunk of samples) are traced in
 // sample passes of at most `scratch` bytes of partial sums each; every pass's reduce continues the
@@ -877,47 +870,14 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     return fail(c, RT_E_INVALID, "bad engine %d", p->engine);
   if (engine == RT_ENGINE_SPLIT && c->split_nt == 0) engine = RT_ENGINE_MEGAKERNEL;  // scene not eligible
 
-  // samples per unit: ~256 units per resident lane, so that a wave's last units (its lanes finish at
-  // different times) cost little, and no unit longer than 16 samples (MI355X: headline frame chunk
-  // 23 -> 8 +0.5 %, final_scene 19 -> 7 +5 %, gen_spheres @ 16 spp 3 -> 1 +24 %; the 1920x1080 @ 2000
-  // spp frames 61 -> 16 +1.5-6 %, tools/gpu_r02chunk3.sh; chunks 25 / 50 on the headline frame -3 / -8 %).
-  // Short units cost only partial-sum traffic (24 B written + read per unit); the scratch they need is
-  // bounded by the sample passes below, not by the unit length.  The wavefront engine keeps its own
-  // unit length (its slots regenerate every iteration anyway).
   const long long lanes = (long long)c->cu_count * std::max(1, c->blocks_per_cu) * c->mk_threads;
-  const int work = std::max(1, count);
-  int chunk = p->sample_chunk;
-  if (chunk == 0 && engine == RT_ENGINE_WAVEFRONT) chunk = kWfDefaultChunk;
-  if (chunk == 0) {
-    const long long want_units = 256 * lanes;
-    long long n_chunks = n_pix > 0 ? (want_units + n_pix - 1) / n_pix : 1;
-    n_chunks = std::max(1LL, std::min<long long>(n_chunks, work));
-    chunk = std::min(16, (int)((work + n_chunks - 1) / n_chunks));
-    // the megakernel's per-block unit segments serve units of >= 4 samples (below): lift a shorter
-    // automatic chunk to 4 while that still leaves >= 100 units per lane (measured: the 4-rank frame
-    // 47.6 -> 47.1 ms; with fewer units per lane — 8 ranks, 57 — the longer units' end costs more than
-    // the segments gain, 24.5 -> 24.9 ms)
-    if (engine == RT_ENGINE_MEGAKERNEL && chunk < 4 && work >= 4 && n_pix > 0 && n_pix * ((work + 3) / 4) >= 100 * lanes)
-      chunk = 4;
-  }
-  chunk = std::max(1, std::min(chunk, work));
-  const int n_chunks = (work + chunk - 1) / chunk;
-
-  // sample passes: at most `budget` bytes of [chunks][pixels][3] f64 partial sums per pass
   long long budget = (long long)(p->scratch_mb > 0 ? p->scratch_mb : kDefaultScratchMiB) << 20;
   if (p->scratch_mb == 0)
     if (const char* e = getenv("SHIRLEY_SCRATCH_MB")) budget = std::max(1LL, atoll(e)) << 20;  // tuning
-  const long long chunk_bytes = std::max<long long>(1, n_pix * 3 * (long long)sizeof(double));
-  int per_pass = (int)std::max(1LL, std::min<long long>(n_chunks, budget / chunk_bytes));
-  if (engine == RT_ENGINE_MEGAKERNEL || engine == RT_ENGINE_SPLIT) {
-    // the megakernel indexes a pass's units and partial slots (n_pix * chunks) in 32 bits
-    const long long max_chunks = n_pix > 0 ? 0xffffffffLL / n_pix : n_chunks;
-    if (max_chunks < 1) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
-    per_pass = (int)std::min<long long>(per_pass, max_chunks);
-  }
-  const int passes = (n_chunks + per_pass - 1) / per_pass;
-  per_pass = (n_chunks + passes - 1) / passes;  // even passes
-  const size_t partial_bytes = (size_t)std::max<long long>(1, n_pix * per_pass * 3) * sizeof(double);
+  const SamplePlan plan = plan_samples(n_pix, count, engine, lanes, p->sample_chunk, budget);
+  if (!plan.ok) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
+  const int chunk = plan.chunk, n_chunks = plan.n_chunks, passes = plan.passes, per_pass = plan.per_pass;
+  const size_t partial_bytes = (size_t)plan.partial_bytes;
   st = ensure(c, c->partial, partial_bytes);
   if (st) return st;
 
@@ -1001,12 +961,9 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     w.n_chunks = c1 - c0;
     w.n_units = (uint64_t)n_pix * (uint64_t)w.n_chunks;
     w.div_unit_tile = make_udiv((uint32_t)w.n_chunks * (uint32_t)kTilePixels);
-    // per-block unit segments (trace.hip, RT_BLOCK_SEGMENTS): one counter per megakernel block, used
-    // for units of >= 4 samples (measured, session T: headline +2 %, gen_spheres +11 %, final_scene
-    // +2.4 %, 2 ranks +2.4 %; with 1- or 2-sample units — small frames, 4 and 8 ranks — the shared
-    // queue is as fast or faster: cfg1 -17 %, the 8-rank frame -6 % with segments)
+    // per-block unit segments (trace.hip, RT_BLOCK_SEGMENTS; plan.h): one counter per megakernel block
     const uint64_t per = (w.n_units + nseg - 1) / nseg;
-    w.n_segs = (engine == RT_ENGINE_MEGAKERNEL && chunk >= 4) ? (uint32_t)nseg : 0u;
+    w.n_segs = plan.segments ? (uint32_t)nseg : 0u;
     w.seg_len = (uint32_t)std::max<uint64_t>(kWave, (per + kWave - 1) / kWave * kWave);
     // the device copy is taken after every field is set (the kernel may read any of them)
     c->host_work[k] = w;

@@ -362,9 +362,10 @@ def test_edge_cases(gpu, engine):
         gpu.render_scanlines(cam, rt.RenderSettings(engine=engine, samples=1), 5, 100)
     if engine in ("megakernel", "split"):
         # 64 pixels x (2^26 + 1) one-sample units (>= 2^32: more than a launch indexes in 32 bits): the call
-        # runs in sample passes (ABI 6) of <= 2 GiB of partial sums (the default bound) — 49 passes of
-        # 1369569 one-sample chunks of 64 pixels — instead of being refused
-        big = gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1, max_reflect=1))
+        # runs in sample passes (ABI 6) of <= 2 GiB of partial sums — 49 passes of 1369569 one-sample
+        # chunks of 64 pixels — instead of being refused
+        big = gpu.render(cam, rt.RenderSettings(engine=engine, samples=(1 << 26) + 1, sample_chunk=1, max_reflect=1,
+                                                scratch_mb=2048))
         c = gpu.counters()
         assert c.passes == 49 and c.scratch_bytes <= 2048 << 20
         assert c.samples == 64 * ((1 << 26) + 1) and np.isfinite(big).all()
