@@ -874,12 +874,17 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
   long long budget = (long long)(p->scratch_mb > 0 ? p->scratch_mb : kDefaultScratchMiB) << 20;
   if (p->scratch_mb == 0)
     if (const char* e = getenv("SHIRLEY_SCRATCH_MB")) budget = std::max(1LL, atoll(e)) << 20;  // tuning
-  const SamplePlan plan = plan_samples(n_pix, count, engine, lanes, p->sample_chunk, budget);
+  SamplePlan plan = plan_samples(n_pix, count, engine, lanes, p->sample_chunk, budget);
   if (!plan.ok) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
+  // a device short of memory gets more, smaller passes instead of a failed call (the frame is the same
+  // for any number of passes)
+  while ((st = ensure(c, c->partial, (size_t)plan.partial_bytes)) == RT_E_OOM && plan.per_pass > 1) {
+    (void)hipGetLastError();
+    plan = plan_samples(n_pix, count, engine, lanes, p->sample_chunk, plan.partial_bytes / 2);
+  }
+  if (st) return st;
   const int chunk = plan.chunk, n_chunks = plan.n_chunks, passes = plan.passes, per_pass = plan.per_pass;
   const size_t partial_bytes = (size_t)plan.partial_bytes;
-  st = ensure(c, c->partial, partial_bytes);
-  if (st) return st;
 
   KParams kp{};
   kp.scene = c->scene;
