@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--timing", action="store_true", help="per-launch HIP-event timing of the wavefront kernels")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of each CPU-baseline leg (full frame at reduced spp; centre rows at full spp)")
+    ap.add_argument("--cpu-config-seconds", type=float, default=5.0,
+                    help="target wall time of each other config's CPU leg (configs 3-5: full frame, reduced spp)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use (cgroup-aware)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
@@ -130,6 +132,18 @@ def host_cpus():
     return usable, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
+def cpu_leg(osc, cam, spp_full, args, threads, seconds, O):
+    """The oracle on `threads` host cores over the full frame at reduced spp: calibrated on one sample per
+    pixel, then sized to ~`seconds` of wall time (at most the config's spp).  (samples, seconds, spp)."""
+    t0 = time.perf_counter()
+    osc.render(cam, O.params(1, args.max_depth, args.seed + 1), threads=threads)
+    per_spp = time.perf_counter() - t0
+    spp = int(max(1, min(spp_full, round(seconds / max(per_spp, 1e-3)))))
+    t0 = time.perf_counter()
+    _, cnt = osc.render(cam, O.params(spp, args.max_depth, args.seed), threads=threads)
+    return cnt.samples, time.perf_counter() - t0, spp
+
+
 def cpu_baseline(scene, cam, args):
     """The oracle (f64 C restatement of the reference path, test infrastructure) timed on the host, on
     every core this process may use (the rayon analogue: row-granular dynamic scheduling), two legs
@@ -142,15 +156,8 @@ def cpu_baseline(scene, cam, args):
     usable, info = host_cpus()
     threads = args.cpu_threads or usable
     W, H = cam.image_width, cam.image_height
-    # calibrate on one sample per pixel, then size each leg to ~cpu_seconds of wall time
-    t0 = time.perf_counter()
-    osc.render(cam, O.params(1, args.max_depth, args.seed + 1), threads=threads)
-    per_spp = time.perf_counter() - t0
-    spp = int(max(1, min(args.spp, round(args.cpu_seconds / max(per_spp, 1e-3)))))
-    t0 = time.perf_counter()
-    _, cnt = osc.render(cam, O.params(spp, args.max_depth, args.seed), threads=threads)
-    dt = time.perf_counter() - t0
-    full = cnt.samples / dt / 1e6
+    n_samples, dt, spp = cpu_leg(osc, cam, args.spp, args, threads, args.cpu_seconds, O)
+    full = n_samples / dt / 1e6
     # centre band at full spp: rows sized from the full-frame rate
     rows = int(max(1, min(H, round(args.cpu_seconds * full * 1e6 / (W * args.spp)))))
     r0 = (H - rows) // 2
@@ -158,7 +165,7 @@ def cpu_baseline(scene, cam, args):
     _, cnt2 = osc.render(cam, O.params(args.spp, args.max_depth, args.seed), r0, r0 + rows, threads=threads)
     dt2 = time.perf_counter() - t0
     return {"value": round(full, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"{args.scene} {W}x{H} @ {spp} spp (full frame, reduced spp; {cnt.samples} samples, "
+            "sample": f"{args.scene} {W}x{H} @ {spp} spp (full frame, reduced spp; {n_samples} samples, "
                       f"{dt:.1f} s wall on {threads} threads; f64 C oracle restating the reference path, "
                       f"-O2 -ffp-contract=off; a proxy: the Rust reference cannot be built here)",
             "centre_rows_leg": {"value": round(cnt2.samples / dt2 / 1e6, 4), "unit": "Msamples/s",
@@ -182,9 +189,13 @@ OTHER_CONFIGS = [
 
 def configs_block(args, dev, torch, rt):
     """One timed full frame of every other BASELINE config on this GPU, after one untimed frame of the
-    same size and spp (it sizes the per-render scratch, so no allocation falls in the timed frame),
-    plus config 1's CPU leg as BASELINE.md specifies it (the oracle, single thread, full frame)."""
+    same size and spp (it sizes the per-render scratch, so no allocation falls in the timed frame), and
+    each config's CPU leg as BASELINE.md specifies it: config 1 the oracle on one thread over the full
+    frame at its spp (BASELINE.md:23); configs 3-5 the oracle on every host core over the full frame at
+    reduced spp (BASELINE.md:24,33-35), with the GPU / CPU ratio of the per-sample rates."""
     out = {}
+    usable, _ = host_cpus()
+    threads = args.cpu_threads or usable
     stream = torch.cuda.current_stream()
     for key, name, width, aspect, spp, note in OTHER_CONFIGS:
         scene = rt.SceneBuilder.builtin(name, args.seed).finalize(args.seed)
@@ -214,6 +225,16 @@ def configs_block(args, dev, torch, rt):
             out[key]["cpu_single_thread"] = {"value": round(cnt.samples / dt / 1e6, 4), "unit": "Msamples/s",
                                              "sample": f"full frame {W}x{H} @ {spp} spp, 1 thread, {dt:.1f} s "
                                                        "(f64 C oracle, a proxy for the Rust reference)"}
+        elif not args.no_cpu:
+            sys.path.insert(0, os.path.join(REPO, "tests"))
+            import oracle_lib as O
+            n, dt, cspp = cpu_leg(O.OracleScene(scene), cam, spp, args, threads, args.cpu_config_seconds, O)
+            rate = n / dt / 1e6
+            out[key]["cpu_all_cores"] = {"value": round(rate, 4), "unit": "Msamples/s", "cores": threads,
+                                         "kind": "port", "spp": cspp,
+                                         "sample": f"full frame {W}x{H} @ {cspp} spp (reduced from {spp}), {n} samples, "
+                                                   f"{dt:.1f} s wall on {threads} threads (f64 C oracle)"}
+            out[key]["gpu_over_cpu"] = round(out[key]["value"] / rate, 1)
     return out
 
 
@@ -251,6 +272,96 @@ def sharded_config5(args, dev, comm, rank, world, torch, dist, rt, width=None, s
                                           "ncclGather of the packed tiles to rank 0",
                                "value": round(W * H * spp / dt / 1e6, 3), "unit": "Msamples/s",
                                "ms_per_frame": round(dt * 1e3, 3), "ranks": world}}
+
+
+def resolve_partition(requested, environ):
+    """The partition rt_render_sharded runs for `requested` (frame_partition in rt_api.cpp): RT_PARTITION_AUTO
+    is tiles unless SHIRLEY_PARTITION=samples overrides it."""
+    if requested != "auto":
+        return requested
+    return "samples" if environ.get("SHIRLEY_PARTITION") == "samples" else "tiles"
+
+
+def compare_frames(ref, got, exact, rel=1e-12):
+    """(ok, detail) of a multi-rank frame against the single-device frame: `exact` bit for bit (tiles:
+    every pixel's sum is computed on one rank with the same unit length), else per channel
+    |got - ref| <= rel * |ref| (samples: the rank-order sum of per-rank shares reassociates the sum)."""
+    import numpy as np
+    ref = np.ascontiguousarray(ref, dtype=np.float64)
+    got = np.ascontiguousarray(got, dtype=np.float64)
+    if ref.shape != got.shape:
+        return False, f"shape {tuple(got.shape)} != {tuple(ref.shape)}"
+    d = np.abs(got - ref)
+    worst = float(np.nanmax(d)) if d.size else 0.0
+    if exact:
+        n = int(np.count_nonzero(ref.view(np.uint64) != got.view(np.uint64)))
+        return n == 0, (f"bit-identical ({ref.size} channels)" if n == 0 else
+                        f"{n} of {ref.size} channels differ, max |d| {worst:.3g}")
+    bad = ~(d <= rel * np.abs(ref))  # (NaN-safe: a NaN difference is bad)
+    n = int(np.count_nonzero(bad))
+    return n == 0, (f"within {rel:g} relative ({ref.size} channels, max |d| {worst:.3g})" if n == 0 else
+                    f"{n} of {ref.size} channels beyond {rel:g} relative, max |d| {worst:.3g}")
+
+
+def sharded_frame(args, dev, comm, rank, world, torch, rt, cam, settings, part):
+    """One multi-rank frame through the job's exchange: rt_render_sharded (RCCL) or, in a gloo rehearsal,
+    the same exchange by torch.distributed (raytracer/parallel.py).  Rank 0 gets the [H][W][3] sums
+    (a CUDA tensor), the other ranks None."""
+    from raytracer.parallel import gather_tiles, reduce_sample_bands, sample_share
+    W, H = cam.image_width, cam.image_height
+    sh = torch.cuda.current_stream().cuda_stream
+    out = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda") if rank == 0 else None
+    if comm is not None:
+        dev.render_sharded(comm, cam, settings, out.data_ptr() if rank == 0 else 0, sh)
+        return out
+    if part == "samples":
+        b, e = sample_share(0, settings.samples, rank, world)
+        local = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+        if e > b:
+            s = rt.RenderSettings(**{**settings.__dict__, "sample_begin": b, "sample_count": e - b, "tile_rank": 0,
+                                     "tile_world": 1})
+            dev.render_device(cam, s, local.data_ptr(), sh)
+        torch.cuda.synchronize()
+        summed = reduce_sample_bands(local.cpu(), world)  # (gloo: host tensors)
+        if rank == 0:
+            out.copy_(summed)
+        return out
+    _, max_tiles = rt.tile_layout(cam, world)
+    packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
+    dev.render_tiles_device(cam, settings, packed.data_ptr(), sh)
+    gathered = gather_tiles(packed, world)
+    if rank == 0:
+        dev.unpack_tiles_device(cam, world, gathered.data_ptr(), out.data_ptr(), sh)
+    return out
+
+
+def multi_rank_check(args, dev, comm, rank, world, torch, rt):
+    """After the timed region at N > 1: a small frame of the headline scene (200x112 @ 8 spp, explicit
+    8-sample units) through the job's exchange with both partitions; rank 0 compares each with the same
+    frame rendered on its device alone (rt_render): tiles bit for bit, samples within 1e-12 relative.
+    The whole-machine loop this replaces is main.rs:117-125.  Returns the JSON block (rank 0; {} elsewhere)."""
+    cam = rt.scene_camera(args.scene, 200, "std16x9")
+    base = dict(samples=8, max_reflect=args.max_depth, seed=args.seed, sample_chunk=8, tile_rank=rank,
+                tile_world=world)
+    frames = {}
+    for part in ("tiles", "samples"):
+        out = sharded_frame(args, dev, comm, rank, world, torch, rt, cam, rt.RenderSettings(**base, partition=part),
+                            part)
+        torch.cuda.synchronize()
+        if rank == 0:
+            frames[part] = out.cpu().numpy()
+    if rank != 0:
+        return {}
+    ref = dev.render(cam, rt.RenderSettings(samples=8, max_reflect=args.max_depth, seed=args.seed, sample_chunk=8))
+    res = {"frame": f"{args.scene} {cam.image_width}x{cam.image_height} @ 8 spp, sample_chunk 8, {world} ranks, "
+                    f"{'rccl' if comm is not None else 'gloo rehearsal'}"}
+    ok_all = True
+    for part in ("tiles", "samples"):
+        ok, detail = compare_frames(ref, frames[part], exact=(part == "tiles"))
+        res[part] = detail
+        ok_all &= ok
+    res["status"] = "ok" if ok_all else "mismatch"
+    return res
 
 
 def valu_block(segments, k_ms, W, H, args):
@@ -321,17 +432,13 @@ def main():
     sh = stream.cuda_stream
     accum = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
     comm = None
-    if world > 1:
-        n_tiles, max_tiles = rt.tile_layout(cam, world)
-        if args.dist_backend == "nccl":
-            # the tile gather runs behind the C ABI (rt_render_sharded: ncclGather to rank 0 over xGMI);
-            # torch.distributed only carries the communicator id, the barriers and the max-over-ranks clock
-            uid = [rt.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            comm = dev.comm_init_rank(uid[0], world, rank)
-        else:
-            packed = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
-            from raytracer.parallel import gather_tiles
+    partition = resolve_partition(args.partition, os.environ)
+    if world > 1 and args.dist_backend == "nccl":
+        # the exchange runs behind the C ABI (rt_render_sharded: ncclGather / ncclAllToAll over xGMI);
+        # torch.distributed only carries the communicator id, the barriers and the max-over-ranks clock
+        uid = [rt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = dev.comm_init_rank(uid[0], world, rank)
 
     # the metric runs from kernel start to the gathered accumulation on the host, so every
     # step ends with the [H][W][3] sums copied into pinned host memory (rank 0: after the gather)
@@ -345,11 +452,11 @@ def main():
             dev.render_device(cam, settings, accum.data_ptr(), sh)
         elif comm is not None:
             dev.render_sharded(comm, cam, settings, accum.data_ptr() if rank == 0 else 0, sh)
-        else:  # gloo rehearsal (ranks sharing one GPU cannot form an RCCL communicator)
-            dev.render_tiles_device(cam, settings, packed.data_ptr(), sh)
-            gathered = gather_tiles(packed, world)
+        else:  # gloo rehearsal (ranks sharing one GPU cannot form an RCCL communicator): the same exchange
+            out = sharded_frame(args, dev, None, rank, world, torch, rt, cam,
+                                rt.RenderSettings(**{**settings.__dict__, "partition": partition}), partition)
             if rank == 0:
-                dev.unpack_tiles_device(cam, world, gathered.data_ptr(), accum.data_ptr(), sh)
+                accum.copy_(out)
         ev_dev[1].record(stream)
         if host_accum is not None:
             host_accum.copy_(accum, non_blocking=True)
@@ -422,7 +529,7 @@ def main():
                    "segments_per_sample": round(float(np.mean(segments)) / max(float(np.mean(samples)), 1.0), 4),
                    "sample_chunk": laps[-1][10], "n_chunks": laps[-1][11], "sample_passes": laps[-1][8],
                    "partial_scratch_bytes": laps[-1][9],
-                   "partition": args.partition if world > 1 else None,
+                   "partition": partition if world > 1 else None,
                    # counted by the instrumented build only (RT_PHASE_TIMING): null here
                    "node_tests_per_segment": round(laps[-1][6] / max(segments[-1], 1), 3) if laps[-1][6] else None,
                    "prim_tests_per_segment": round(laps[-1][7] / max(segments[-1], 1), 3) if laps[-1][7] else None},
@@ -436,6 +543,11 @@ def main():
                      "valu": valu_block(seg, k_ms, W, H, args) if world == 1 else None},
         "cpu_baseline": None,
     }
+    mrc = None
+    if world > 1:  # (after the timed region: the exchange of this job checked against one device's frame)
+        mrc = multi_rank_check(args, dev, comm, rank, world, torch, rt)
+        if rank == 0:
+            line["multi_rank_check"] = mrc
     if rank == 0 and world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(scene, cam, args)
     if world == 1 and not args.no_configs:  # (after the timed region; the headline scene is replaced)
@@ -452,6 +564,8 @@ def main():
     dev.close()
     if world > 1:
         dist.destroy_process_group()
+    if mrc and mrc.get("status") != "ok":
+        sys.exit(f"bench.py: multi-rank frame differs from the single-device frame: {mrc}")
 
 
 if __name__ == "__main__":

@@ -321,9 +321,14 @@ int rt_scene_hit_ex(rt_ctx* ctx, const double* rays, int32_t n, double t_min, do
  * every rank renders all pixels for a share of the samples (RT_PARTITION_SAMPLES, see above).  The
  * counter RNG is keyed by the global pixel and sample, so a tile-sharded frame is bit-identical for every
  * world size given an explicit sample_chunk (the automatic chunk follows the rank's pixel count).  Every
- * ctx must hold the same scene: the calls compare the scenes' digests (rt_scene_digest) across ranks
- * first and fail with RT_E_INVALID on a mismatch (rt_render_sharded: an 8-byte all-gather; the call
- * synchronises the host with the stream for it).  Replaces the
+ * ctx must hold the same scene and every rank must pass the same call arguments: rt_render_sharded
+ * all-gathers each rank's (scene digest, call key) — the key hashes the resolved partition and sample
+ * range, samples, seed, max_depth, sample_chunk and the camera — and fails with RT_E_INVALID on every rank
+ * alike on a mismatch, before any collective of the frame.  The agreed key is cached on the communicator:
+ * a call whose key equals it does no exchange and no host synchronisation (a loop of frames stays
+ * asynchronous); ranks changing scene or arguments together re-check on that call.  (A rank that changes
+ * them alone re-checks while the others proceed to the frame's collectives: that misuse stalls instead
+ * of failing.)  rt_render_multi compares the digests on the host.  Replaces the
  * reference's whole-machine rayon loop over scanlines (main.rs:92-126).  RCCL is loaded on first use
  * (dlopen "librccl.so.1": the copy already in the process if any); without it these calls return
  * RT_E_RCCL.
@@ -336,8 +341,8 @@ typedef struct rt_comm rt_comm;
 int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
 int rt_comm_init_rank(rt_ctx* ctx, const uint8_t id[RT_COMM_ID_BYTES], int32_t world, int32_t rank, rt_comm** out);
 int rt_comm_destroy(rt_comm* comm);
-/* One rank's share of a sharded frame, asynchronous on `stream` (NULL: the ctx's stream) after the scene
- * digest check: render the rank's share (params->partition: its tiles, or all pixels for its samples;
+/* One rank's share of a sharded frame, asynchronous on `stream` (NULL: the ctx's stream) after the
+ * cross-rank check above: render the rank's share (params->partition: its tiles, or all pixels for its samples;
  * params->tile_rank / tile_world are ignored: the communicator's rank and size are used), exchange, and on
  * rank 0 write accum_dev ([H][W][3] f64 sums on its device; NULL on the other ranks).  The sample range of
  * params (sample_begin / sample_count) is the frame's; a sample partition splits it.  Every rank of the

@@ -58,6 +58,97 @@ struct Args {
   std::exit(2);
 }
 
+// A checkpoint's identity (--dump-accum FILE + FILE.json, --resume FILE): its sums are the per-pixel sums
+// of samples [0, samples_done) of one frame, so a resume must render that same frame — the same scene
+// (rt_scene_digest_host of the description and BVH builder), camera (FNV-1a over its fields), seed,
+// max_depth and sample_chunk (the unit length decides the sums' bits) — and may only add samples.
+struct Checkpoint {
+  long long samples_done = -1, samples = -1, width = -1, height = -1, max_depth = -1, sample_chunk = -1;
+  unsigned long long seed = 0, scene = 0, camera = 0;
+};
+
+unsigned long long camera_digest(const rt_camera& c) {
+  unsigned long long h = 14695981039346656037ull;
+  auto bytes = [&](const void* p, size_t n) {
+    for (size_t i = 0; i < n; ++i) h = (h ^ static_cast<const unsigned char*>(p)[i]) * 1099511628211ull;
+  };
+  bytes(&c.image_width, sizeof c.image_width); bytes(&c.image_height, sizeof c.image_height);
+  bytes(&c.height, sizeof c.height); bytes(&c.width, sizeof c.width); bytes(&c.focal_length, sizeof c.focal_length);
+  bytes(&c.has_lens, sizeof c.has_lens); bytes(&c.lens_radius, sizeof c.lens_radius);
+  bytes(c.origin, sizeof c.origin); bytes(c.w, sizeof c.w); bytes(c.u, sizeof c.u); bytes(c.v, sizeof c.v);
+  bytes(&c.focus_length, sizeof c.focus_length); bytes(&c.time0, sizeof c.time0); bytes(&c.time1, sizeof c.time1);
+  return h;
+}
+
+Checkpoint checkpoint_of(const Args& a, const rt_scene_desc* desc, const rt_camera& cam, int samples, int done) {
+  Checkpoint k;
+  k.samples_done = done;
+  k.samples = samples;
+  k.width = cam.image_width;
+  k.height = cam.image_height;
+  k.max_depth = a.max_reflect;
+  k.sample_chunk = a.sample_chunk;
+  k.seed = a.seed;
+  uint64_t d = 0;
+  if (rt_scene_digest_host(desc, a.bvh == "sah" ? RT_BVH_SAH : RT_BVH_REFERENCE, &d) == RT_OK) k.scene = d;
+  k.camera = camera_digest(cam);
+  return k;
+}
+
+void write_checkpoint(const std::string& path, const std::vector<double>& accum, const Checkpoint& k) {
+  std::ofstream f(path, std::ios::binary);
+  f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
+  char digests[80];
+  std::snprintf(digests, sizeof digests, "\"scene_digest\": \"%016llx\", \"camera_digest\": \"%016llx\"", k.scene,
+                k.camera);
+  std::ofstream fj(path + ".json");
+  fj << "{\"samples_done\": " << k.samples_done << ", \"samples\": " << k.samples << ", \"width\": " << k.width
+     << ", \"height\": " << k.height << ", \"seed\": " << k.seed << ", \"max_depth\": " << k.max_depth
+     << ", \"sample_chunk\": " << k.sample_chunk << ", " << digests << "}\n";
+}
+
+// FILE.json's fields (the writer's own flat format); false when one is missing
+bool read_checkpoint(const std::string& path, Checkpoint* k) {
+  std::ifstream fj(path + ".json");
+  const std::string js((std::istreambuf_iterator<char>(fj)), std::istreambuf_iterator<char>());
+  auto field = [&](const char* name, bool hex, unsigned long long* out) {
+    const std::string key = std::string("\"") + name + "\":";
+    const size_t at = js.find(key);
+    if (at == std::string::npos) return false;
+    const char* s = js.c_str() + at + key.size();
+    while (*s == ' ' || *s == '"') ++s;
+    char* end = nullptr;
+    *out = std::strtoull(s, &end, hex ? 16 : 10);
+    return end != s;
+  };
+  unsigned long long v[9];
+  const char* names[9] = {"samples_done", "samples", "width", "height", "max_depth", "sample_chunk", "seed",
+                          "scene_digest", "camera_digest"};
+  for (int i = 0; i < 9; ++i)
+    if (!field(names[i], i >= 7, &v[i])) return false;
+  k->samples_done = (long long)v[0]; k->samples = (long long)v[1]; k->width = (long long)v[2];
+  k->height = (long long)v[3]; k->max_depth = (long long)v[4]; k->sample_chunk = (long long)v[5];
+  k->seed = v[6]; k->scene = v[7]; k->camera = v[8];
+  return true;
+}
+
+// Why checkpoint `c` cannot be continued as frame `want` (empty: it can)
+std::string checkpoint_mismatch(const Checkpoint& c, const Checkpoint& want) {
+  char m[160] = "";
+  if (c.scene != want.scene) std::snprintf(m, sizeof m, "scene %016llx, this run %016llx", c.scene, want.scene);
+  else if (c.width != want.width || c.height != want.height)
+    std::snprintf(m, sizeof m, "%lldx%lld, this run %lldx%lld", c.width, c.height, want.width, want.height);
+  else if (c.camera != want.camera) std::snprintf(m, sizeof m, "another camera");
+  else if (c.seed != want.seed) std::snprintf(m, sizeof m, "seed %llu, this run %llu", c.seed, want.seed);
+  else if (c.max_depth != want.max_depth)
+    std::snprintf(m, sizeof m, "max_depth %lld, this run %lld", c.max_depth, want.max_depth);
+  else if (c.sample_chunk != want.sample_chunk)
+    std::snprintf(m, sizeof m, "sample_chunk %lld, this run %lld", c.sample_chunk, want.sample_chunk);
+  else if (c.samples_done < 0 || c.samples_done > want.samples)
+    std::snprintf(m, sizeof m, "it covers %lld samples, this run renders %lld", c.samples_done, want.samples);
+  return m;
+}
+
 // --gpus N > 1: one ctx per device, the scene uploaded to each, rt_render_multi (tiles + RCCL gather
 // to the first device), to_image on the host.
 int render_scene_multi(const Args& a, const rt_scene_desc* desc, const rt_camera& cam, int samples) {
@@ -100,10 +191,7 @@ int render_scene_multi(const Args& a, const rt_scene_desc* desc, const rt_camera
     std::fprintf(stderr, "INFO %d GPUs: render %.1f ms (incl. gather and copy-back): %.1f Msamples/s\n", a.gpus, ms,
                  (double)cam.image_width * cam.image_height * samples / (ms * 1e3));
   rt_tonemap(accum.data(), cam.image_width, cam.image_height, samples, rgb.data());  // image.rs:31-44
-  if (!a.dump_accum.empty()) {
-    std::ofstream f(a.dump_accum, std::ios::binary);
-    f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
-  }
+  if (!a.dump_accum.empty()) write_checkpoint(a.dump_accum, accum, checkpoint_of(a, desc, cam, samples, samples));
   if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
     std::fprintf(stderr, "error: %s\n", sh_last_error());
     return done(1);
@@ -149,22 +237,22 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
     accum.assign(n, 0.0);
     int done = 0;
     if (!a.resume.empty()) {
-      std::ifstream fj(a.resume + ".json");
-      std::string js((std::istreambuf_iterator<char>(fj)), std::istreambuf_iterator<char>());
-      const size_t k = js.find("\"samples_done\":");
+      Checkpoint ck;
       std::ifstream f(a.resume, std::ios::binary);
       f.read((char*)accum.data(), (std::streamsize)(n * sizeof(double)));
-      if (k == std::string::npos || !f || f.gcount() != (std::streamsize)(n * sizeof(double))) {
-        std::fprintf(stderr, "error: %s is not a checkpoint of this frame\n", a.resume.c_str());
+      if (!read_checkpoint(a.resume, &ck) || !f || f.gcount() != (std::streamsize)(n * sizeof(double)) ||
+          f.peek() != std::char_traits<char>::eof()) {
+        std::fprintf(stderr, "error: %s is not a checkpoint of this frame size\n", a.resume.c_str());
         rt_destroy(ctx);
         return 1;
       }
-      done = std::atoi(js.c_str() + k + 15);
-      if (done < 0 || done > samples) {
-        std::fprintf(stderr, "error: checkpoint covers %d samples of %d\n", done, samples);
+      const std::string why = checkpoint_mismatch(ck, checkpoint_of(a, desc, cam, samples, 0));
+      if (!why.empty()) {
+        std::fprintf(stderr, "error: %s is a checkpoint of another frame: %s\n", a.resume.c_str(), why.c_str());
         rt_destroy(ctx);
         return 1;
       }
+      done = (int)ck.samples_done;
     }
     std::vector<double> part(n);
     const int ranges = std::max(1, a.progressive);
@@ -181,13 +269,7 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
       }
       for (size_t i = 0; i < n; ++i) accum[i] += part[i];
       rt_tonemap(accum.data(), cam.image_width, cam.image_height, e, rgb.data());
-      if (!a.dump_accum.empty()) {
-        std::ofstream f(a.dump_accum, std::ios::binary);
-        f.write((const char*)accum.data(), (std::streamsize)(n * sizeof(double)));
-        std::ofstream fj(a.dump_accum + ".json");
-        fj << "{\"samples_done\": " << e << ", \"samples\": " << samples << ", \"width\": " << cam.image_width
-           << ", \"height\": " << cam.image_height << ", \"seed\": " << a.seed << "}\n";
-      }
+      if (!a.dump_accum.empty()) write_checkpoint(a.dump_accum, accum, checkpoint_of(a, desc, cam, samples, e));
       if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
         std::fprintf(stderr, "error: %s\n", sh_last_error());
         rt_destroy(ctx);
@@ -243,13 +325,8 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
                  std::chrono::duration<double, std::milli>(t1 - t0).count(), ms, cnt.kernel_ms, cnt.reduce_ms, msamp,
                  (double)cnt.segments / (double)(cnt.samples ? cnt.samples : 1));
   rt_destroy(ctx);
-  if (!a.dump_accum.empty()) {  // a complete checkpoint (--resume reads FILE.json's samples_done)
-    std::ofstream f(a.dump_accum, std::ios::binary);
-    f.write((const char*)accum.data(), (std::streamsize)(accum.size() * sizeof(double)));
-    std::ofstream fj(a.dump_accum + ".json");
-    fj << "{\"samples_done\": " << samples << ", \"samples\": " << samples << ", \"width\": " << cam.image_width
-       << ", \"height\": " << cam.image_height << ", \"seed\": " << a.seed << "}\n";
-  }
+  if (!a.dump_accum.empty())  // a complete checkpoint
+    write_checkpoint(a.dump_accum, accum, checkpoint_of(a, desc, cam, samples, samples));
   if (sh_write_png(a.output.c_str(), rgb.data(), cam.image_width, cam.image_height)) {
     std::fprintf(stderr, "error: %s\n", sh_last_error());
     return 1;

@@ -69,6 +69,10 @@ struct DevBuf {
 struct rt_comm {
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0, device = 0;
+  // the call key (scene digest + resolved partition, sample range and the render arguments) every rank
+  // last agreed on; rt_render_sharded exchanges keys only when this rank's key differs from it
+  bool verified = false;
+  uint64_t verified_key = 0;
 };
 
 struct rt_ctx {
@@ -79,7 +83,7 @@ struct rt_ctx {
   // scene
   bool have_scene = false;
   DScene scene{};
-  DevBuf nodes, nodes4, prims, mats, texs, perlin, images, texels, exts;
+  DevBuf nodes, nodes4, prims, mats, texs, perlin, texels, exts;
   rt_scene_stats stats{};
   int blocks_per_cu = 0;
   int mk_threads = kTraceThreads;  // megakernel block size (kTraceThreadsWide: whole BVH in LDS)
@@ -103,7 +107,8 @@ struct rt_ctx {
   int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0, last_passes = 0;
   uint64_t last_slots = 0, last_scratch = 0;
   std::vector<hipEvent_t> pass_ev;   // before / after the trace launch of each sample pass
-  DCamera host_cam{};                // host sources of the device copies (KParams.cam_const / work_const)
+  DCamera host_cam{};
+  DScene host_scene{};                // host sources of the device copies (KParams.cam_const / work_const)
   std::vector<DWork> host_work;
   uint64_t digest = 0;               // rt_scene_digest of the uploaded scene
   uint64_t host_samples = 0;  // samples of a frame served without a trace kernel (max_depth == 0)
@@ -904,14 +909,19 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
   kp.partial = static_cast<double*>(c->partial.p);
   kp.counters = static_cast<DCounters*>(c->counters.p);
 
-  // device copies of the camera and of each pass's work descriptor (KParams.cam_const / work_const);
-  // their host sources stay alive in the ctx until the next call
-  st = ensure(c, c->kcam, 2 * sizeof(DCamera) + (size_t)passes * sizeof(DWork));
+  // device copies of the camera, the scene record and each pass's work descriptor (KParams.cam_const /
+  // scene_const / work_const), 16-B aligned; their host sources stay alive in the ctx until the next call
+  constexpr size_t kCamBytes = (sizeof(DCamera) + 15) / 16 * 16, kSceneBytes = (sizeof(DScene) + 15) / 16 * 16;
+  st = ensure(c, c->kcam, kCamBytes + kSceneBytes + (size_t)passes * sizeof(DWork));
   if (st) return st;
   c->host_cam = kp.cam;
+  c->host_scene = kp.scene;
   c->host_work.assign(passes, DWork{});
   HIP_TRY(c, hipMemcpyAsync(c->kcam.p, &c->host_cam, sizeof(DCamera), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(static_cast<char*>(c->kcam.p) + kCamBytes, &c->host_scene, sizeof(DScene),
+                            hipMemcpyHostToDevice, s));
   kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
+  kp.scene_const = (uint64_t)(uintptr_t)(static_cast<char*>(c->kcam.p) + kCamBytes);
 
   const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
   {
@@ -966,13 +976,13 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     w.n_chunks = c1 - c0;
     w.n_units = (uint64_t)n_pix * (uint64_t)w.n_chunks;
     w.div_unit_tile = make_udiv((uint32_t)w.n_chunks * (uint32_t)kTilePixels);
-    // per-block unit segments (trace.hip, RT_BLOCK_SEGMENTS; plan.h): one counter per megakernel block
+    // per-block unit segments (trace.hip; plan.h): one counter per megakernel block
     const uint64_t per = (w.n_units + nseg - 1) / nseg;
     w.n_segs = plan.segments ? (uint32_t)nseg : 0u;
     w.seg_len = (uint32_t)std::max<uint64_t>(kWave, (per + kWave - 1) / kWave * kWave);
     // the device copy is taken after every field is set (the kernel may read any of them)
     c->host_work[k] = w;
-    void* kwork = static_cast<char*>(c->kcam.p) + 2 * sizeof(DCamera) + (size_t)k * sizeof(DWork);  // (16-B aligned)
+    void* kwork = static_cast<char*>(c->kcam.p) + kCamBytes + kSceneBytes + (size_t)k * sizeof(DWork);
     HIP_TRY(c, hipMemcpyAsync(kwork, &c->host_work[k], sizeof(DWork), hipMemcpyHostToDevice, s));
     kp.work_const = (uint64_t)(uintptr_t)kwork;
     HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t)), s));
@@ -1044,7 +1054,7 @@ int rt_destroy(rt_ctx* c) {
   if (!c) return RT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->images, &c->texels, &c->exts, &c->partial, &c->kcam,
+  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->texels, &c->exts, &c->partial, &c->kcam,
                     &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters, &c->packed, &c->gathered,
                     &c->parts, &c->band, &c->digests})
     release(*b);
@@ -1097,7 +1107,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     // a sphere's 1 / radius (sphere.rs:48 `scale(1.0 / self.radius)`), the same IEEE quotient the device
     // would compute per hit record; p[4] is otherwise unused by spheres
     if (q.kind == kPrimSphere || q.kind == kPrimMovingSphere) q.p[4] = 1.0 / q.p[3];
-    q.material = o.material | (d->materials[o.material].kind == RT_MAT_DIELECTRIC ? kPrimMatDielectric : 0);
+    q.material = o.material;
     if (is_extended(o)) {
       if (exts.size() >= (1u << (31 - kPrimExtShift)))
         return fail(c, RT_E_UNSUPPORTED, "too many extended objects");
@@ -1137,7 +1147,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     q.odd = t.odd;
     q.even = t.even;
     q.table = t.table;
-    for (int k = 0; k < 3; ++k) q.color[k] = t.color[k];
+    if (t.kind != RT_TEX_IMAGE)
+      for (int k = 0; k < 3; ++k) q.color[k] = t.color[k];
     q.scale = t.scale;
   }
   std::vector<DPerlin> perl(std::max(1, d->n_perlin));
@@ -1147,12 +1158,12 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     std::memcpy(perl[i].perm_y, d->perlin[i].perm_y, sizeof perl[i].perm_y);
     std::memcpy(perl[i].perm_z, d->perlin[i].perm_z, sizeof perl[i].perm_z);
   }
-  std::vector<DImage> imgs(std::max(1, d->n_images));
+  // every image's RGB8 texels in one pool; an image texture's DTex points at its image (below, once the
+  // pool is on the device)
+  std::vector<size_t> img_off(std::max(1, d->n_images));
   std::vector<uint8_t> texels;
   for (int i = 0; i < d->n_images; ++i) {
-    imgs[i].width = d->images[i].width;
-    imgs[i].height = d->images[i].height;
-    imgs[i].offset = (int64_t)texels.size();
+    img_off[i] = texels.size();
     size_t nb = (size_t)d->images[i].width * d->images[i].height * 3;
     texels.insert(texels.end(), d->images[i].rgb, d->images[i].rgb + nb);
   }
@@ -1177,10 +1188,16 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   }
   if ((st = upload(c, c->prims, prims.data(), prims.size() * sizeof(DPrim)))) return st;
   if ((st = upload(c, c->mats, mats.data(), mats.size() * sizeof(DMat)))) return st;
+  if ((st = upload(c, c->texels, texels.data(), texels.size()))) return st;
+  for (int i = 0; i < d->n_textures; ++i)
+    if (d->textures[i].kind == RT_TEX_IMAGE) {
+      const int im = d->textures[i].table;  // (validated: a texture's image index is in range)
+      texs[i].img.texels = static_cast<const uint8_t*>(c->texels.p) + img_off[im];
+      texs[i].img.width = d->images[im].width;
+      texs[i].img.height = d->images[im].height;
+    }
   if ((st = upload(c, c->texs, texs.data(), texs.size() * sizeof(DTex)))) return st;
   if ((st = upload(c, c->perlin, perl.data(), perl.size() * sizeof(DPerlin)))) return st;
-  if ((st = upload(c, c->images, imgs.data(), imgs.size() * sizeof(DImage)))) return st;
-  if ((st = upload(c, c->texels, texels.data(), texels.size()))) return st;
   if (!exts.empty()) {
     if ((st = upload(c, c->exts, exts.data(), exts.size() * sizeof(DExt)))) return st;
   } else {
@@ -1204,8 +1221,6 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.mats = static_cast<const DMat*>(c->mats.p);
   S.texs = static_cast<const DTex*>(c->texs.p);
   S.perlin = static_cast<const DPerlin*>(c->perlin.p);
-  S.images = static_cast<const DImage*>(c->images.p);
-  S.texels = static_cast<const uint8_t*>(c->texels.p);
   S.exts = exts.empty() ? nullptr : static_cast<const DExt*>(c->exts.p);
   S.time0 = S.time1 = 0.0;  // the shutter comes with each render call's camera
   S.n_nodes = (int32_t)nodes.size();
@@ -1303,7 +1318,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->stats.origin_limit = S.origin_limit;
   c->stats.device_bytes = (int64_t)(nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim) +
                                     mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex) +
-                                    perl.size() * sizeof(DPerlin) + imgs.size() * sizeof(DImage) + texels.size());
+                                    perl.size() * sizeof(DPerlin) + texels.size());
   c->digest = scene_digest(d, builder);
   c->have_scene = true;
   return RT_OK;
@@ -1457,17 +1472,17 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
   }
 #ifdef RT_PHASE_TIMING
   {
-    double ph[3] = {0, 0, 0};
+    double ph[kPhBuckets] = {};
     for (const DCounters& k : dc)
-      for (int i = 0; i < 3; ++i) ph[i] += (double)k.pad[i];
-    const double tot = ph[0] + ph[1] + ph[2];
-    fprintf(stderr, "[phase] regen %.3f trav %.3f shade %.3f (wave-cycles %.4g)\n", ph[0] / tot, ph[1] / tot,
-            ph[2] / tot, tot);
-    double lane = 0, wave = 0;
-    for (const DCounters& k : dc) {
-      lane += (double)k.pad[3];
-      wave += (double)k.pad[4];
-    }
+      for (int i = 0; i < kPhBuckets; ++i) ph[i] += (double)k.pad[i];
+    const int order[] = {kPhTrav, kPhRecord, kPhRegen, kPhMarble, kPhDraws, kPhCamera, kPhShade, kPhTail};
+    const char* names[] = {"trav", "record", "regen", "marble", "draws", "camera", "shade", "tail"};
+    double tot = 0;
+    for (int b : order) tot += ph[b];
+    fprintf(stderr, "[phase] wave-time fractions:");
+    for (int i = 0; i < 8; ++i) fprintf(stderr, " %s %.4f", names[i], ph[order[i]] / tot);
+    fprintf(stderr, " (wave-cycles %.4g)\n", tot);
+    const double lane = ph[kPhLaneSteps], wave = ph[kPhWaveSteps];
     fprintf(stderr, "[phase] traversal lane steps %.4g, wave steps %.4g, SIMD utilisation %.3f\n", lane, wave,
             lane / (64.0 * wave));
     phase_counters_dump();
@@ -1654,22 +1669,68 @@ int shard_unpack(rt_ctx* c, const rt_camera* cam, int part, int world, double* a
   return RT_OK;
 }
 
-// Every rank's scene digest must be the same: an 8-byte all-gather, read on the host.  All ranks see the
-// same gathered digests, so a mismatch fails on every rank alike (no rank is left waiting in a collective).
-int check_digests(rt_ctx* c, rt_comm* m, hipStream_t s) {
-  const size_t bytes = (size_t)m->world * sizeof(uint64_t);
-  int st = ensure(c, c->digests, bytes + sizeof(uint64_t));
+// What every rank of a sharded frame must agree on: the scene (its digest) and the arguments that decide
+// the collectives' shapes and the frame's bits — the resolved partition, the resolved sample range, samples,
+// seed, max_depth, sample_chunk and the camera (field by field, no padding hashed).  FNV-1a, 64 bits.
+uint64_t call_key(const rt_ctx* c, const rt_camera* cam, const rt_render_params* p, int part, const SampleRange& R) {
+  Fnv1a f;
+  f.val(c->digest);
+  f.val(part);
+  f.val(R.begin);
+  f.val(R.end);
+  f.val(p->samples);
+  f.val(p->seed);
+  f.val(p->max_depth);
+  f.val(p->sample_chunk);
+  f.val(cam->image_width);
+  f.val(cam->image_height);
+  f.val(cam->height);
+  f.val(cam->width);
+  f.val(cam->focal_length);
+  f.val(cam->has_lens);
+  f.val(cam->lens_radius);
+  f.bytes(cam->origin, sizeof cam->origin);
+  f.bytes(cam->w, sizeof cam->w);
+  f.bytes(cam->u, sizeof cam->u);
+  f.bytes(cam->v, sizeof cam->v);
+  f.val(cam->focus_length);
+  f.val(cam->time0);
+  f.val(cam->time1);
+  return f.h;
+}
+
+// Every rank must render the same scene with the same call key: a 16-byte-per-rank all-gather of (scene
+// digest, key), read on the host.  All ranks see the same gathered words, so a mismatch fails on every rank
+// alike (RT_E_INVALID naming the first differing rank), and no collective of the frame is issued.  The
+// agreed key is cached on the communicator: a rank whose key equals it skips the exchange (no host round
+// trip in a steady-state loop of frames).  Every rank of a correct program changes its key in the same call
+// (a new scene on every rank, new arguments on every rank), so all ranks exchange together; a rank that
+// changes its key alone exchanges while the others go on to the frame's collectives, which RCCL cannot
+// match — the check turns a silently wrong frame into a stall in that misuse (shirley_rt.h).
+int check_call_key(rt_ctx* c, rt_comm* m, uint64_t key, hipStream_t s) {
+  if (m->verified && m->verified_key == key) return RT_OK;
+  const size_t bytes = (size_t)m->world * 2 * sizeof(uint64_t);
+  int st = ensure(c, c->digests, bytes + 2 * sizeof(uint64_t));
   if (st) return st;
   uint64_t* d = static_cast<uint64_t*>(c->digests.p);
-  HIP_TRY(c, hipMemcpyAsync(d + m->world, &c->digest, sizeof(uint64_t), hipMemcpyHostToDevice, s));
-  RCCL_TRY(c, rccl().AllGather(d + m->world, d, 1, ncclUint64, m->comm, s));
-  std::vector<uint64_t> all(m->world);
+  const uint64_t mine[2] = {c->digest, key};
+  HIP_TRY(c, hipMemcpyAsync(d + 2 * m->world, mine, sizeof mine, hipMemcpyHostToDevice, s));
+  RCCL_TRY(c, rccl().AllGather(d + 2 * m->world, d, 2, ncclUint64, m->comm, s));
+  std::vector<uint64_t> all(2 * (size_t)m->world);
   HIP_TRY(c, hipMemcpyAsync(all.data(), d, bytes, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   for (int r = 0; r < m->world; ++r)
-    if (all[r] != all[0])
+    if (all[2 * r] != all[0])
       return fail(c, RT_E_INVALID, "scene mismatch across ranks: rank %d holds scene %016llx, rank 0 %016llx", r,
-                  (unsigned long long)all[r], (unsigned long long)all[0]);
+                  (unsigned long long)all[2 * r], (unsigned long long)all[0]);
+  for (int r = 0; r < m->world; ++r)
+    if (all[2 * r + 1] != all[1])
+      return fail(c, RT_E_INVALID,
+                  "render arguments differ across ranks (partition, sample range, samples, seed, max_depth, "
+                  "sample_chunk or camera): rank %d key %016llx, rank 0 %016llx",
+                  r, (unsigned long long)all[2 * r + 1], (unsigned long long)all[1]);
+  m->verified = true;
+  m->verified_key = key;
   return RT_OK;
 }
 
@@ -1731,10 +1792,13 @@ int rt_render_sharded(rt_ctx* c, rt_comm* m, const rt_camera* cam, const rt_rend
   int part = 0;
   int st = frame_partition(c, p, m->world, &part);
   if (st) return st;
+  if ((st = check_render_args(c, cam, p))) return st;
+  SampleRange R;
+  if ((st = resolve_range(c, p, &R))) return st;
   hipStream_t s;
   resolve_stream(c, stream, &s);
   HIP_TRY(c, hipSetDevice(c->device));
-  if ((st = check_digests(c, m, s))) return st;
+  if ((st = check_call_key(c, m, call_key(c, cam, p, part, R), s))) return st;
   size_t count = 0;
   if ((st = shard_render(c, cam, p, part, m->world, m->rank, s, &count))) return st;
   if (part == RT_PARTITION_SAMPLES) {

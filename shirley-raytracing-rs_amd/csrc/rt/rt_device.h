@@ -114,10 +114,13 @@ __device__ __forceinline__ uint32_t udiv(uint32_t n, const UDiv& D) {
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
+#ifndef RT_PHILOX_ROUNDS  // (timing experiments only: the oracle and every test use 10)
+#define RT_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ void philox10(uint32_t& c0, uint32_t& c1, uint32_t& c2, uint32_t& c3, uint32_t k0,
                                          uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < RT_PHILOX_ROUNDS; ++r) {
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
@@ -203,9 +206,6 @@ __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t
 // ------------------------------------------------------------------------------------------
 // intersection (t only during traversal; the full hit record is rebuilt for the winner)
 // ------------------------------------------------------------------------------------------
-#ifndef RT_POP_SKIP
-#define RT_POP_SKIP 0
-#endif
 // ------------------------------------------------------------------------------------------
 // aabb.rs:62-79 hit2, per axis: t0 = (min - o) * inv, t1 = (max - o) * inv, swapped when inv < 0,
 // t_min = t0 > t_min ? t0 : t_min, t_max = t1 < t_max ? t1 : t_max, miss when t_max <= t_min
@@ -763,7 +763,11 @@ __device__ __forceinline__ void ph_count(int i) {
     atomicAdd(&g_phase_ctr[2 * i + 1], 1ull);
   }
 }
+#ifndef RT_PHASE_NO_EVENTS
 #define PH_COUNT(i) ph_count(i)
+#else  // (clock stamps only: the event atomics would dominate the phase clocks)
+#define PH_COUNT(i)
+#endif
 #else
 #define PH_COUNT(i)
 #endif
@@ -771,8 +775,10 @@ __device__ __forceinline__ void ph_count(int i) {
 // build only (they cost the production megakernel 0.5 %: ~15 VALU per iteration and two registers).
 #ifdef RT_PHASE_TIMING
 #define RT_STAT(x) x
+#define RT_STAT_ARG(x) , x
 #else
 #define RT_STAT(x)
+#define RT_STAT_ARG(x)
 #endif
 #ifdef RT_TIMELINE
 // timeline build: per-wave start, unit-pool-exhausted and exit times (s_memrealtime, 100 MHz)
@@ -1093,9 +1099,10 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   if (p2 <= lim) { stk[sp] = top; sp += STRIDE; top = p2; }
   if (p1 <= lim) { stk[sp] = top; sp += STRIDE; top = p1; }
   if (p0 <= lim) return (int)(p0 & km);
-#if RT_POP_SKIP
-  // (A/B switch) culled entries are skipped in a loop with a single-compare exit (lim < e < ~0u as one
-  // unsigned range test); the accepted entry is then popped once
+  // Culled entries are skipped in a loop with a single-compare exit (lim < e < ~0u as one unsigned
+  // range test: 4 VALU + 3 SALU per trip instead of 11 + 7 for a test-pop-compare loop; +0.4 % on the
+  // headline); the accepted entry is then popped once.  Same entries popped in the same
+  // order as popping one at a time.
   const unsigned lo = lim + 1u, span = ~0u - lo;
   unsigned e = top;
   while (e - lo < span) {
@@ -1110,16 +1117,6 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   sp -= STRIDE;  // e is a real entry: the ~0u sentinel lies below it
   top = stk[sp];
   return (int)(e & km);
-#else
-  for (;;) {
-    PH_COUNT(5);
-    const unsigned e = top;
-    if (e == ~0u) return -1;
-    sp -= STRIDE;
-    top = stk[sp];
-    if (e <= lim) return (int)(e & km);
-  }
-#endif
 }
 template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
@@ -1170,90 +1167,6 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
 #endif
     node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, ra, ra_ok, t_min, node, t_best, tmaxf, best,
                                 face_best, sp, top, stk, rk, seed, visits, ptests);
-  }
-  return best;
-}
-
-// traverse4 with dielectric chaining, for the megakernel on reference scenes.  A wave
-// runs its traversal loop until its slowest lane is done; a lane whose segment ends early — most often
-// a hop through the ground's glass coat (a RectBox of ir 1: one node visit) — would sit out the rest of
-// that loop and then one whole iteration of shading per hop.  Here a lane whose closest hit is a
-// dielectric and whose path goes on (depth_left > 1) scatters right away — the reference's dielectric
-// step (dielectric.rs:21-49, the same operations and draws as shade_factor with draws_coop: the uniform
-// from rng_next, drawn only without total internal reflection; attenuation 1, no emission) — and
-// starts the next segment's traversal in the same loop, on a lane that was idle.  At most CHAIN such
-// segments per call; `chained` counts them.  Returns the closest hit of the last segment, whose ray is
-// then (o, d); the caller shades it as before.
-__device__ __forceinline__ double pow5(double x);  // (below, with the materials)
-// dielectric.rs:15-19 (Schlick), inlined here (the shading's copy is out of line: `reflectance`)
-__device__ __forceinline__ double reflectance_inl(double cosine, double ref_idx) {
-  double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
-  r0 = r0 * r0;
-  return r0 + (1.0 - r0) * pow5(1.0 - cosine);
-}
-// Chaining is allowed after a traversal of at most this many node visits (RT_CHAIN_STEPS): such
-// segments end together early in the loop, so one pass of the dielectric code serves many lanes.
-#ifndef RT_CHAIN_STEPS
-#define RT_CHAIN_STEPS 1
-#endif
-template <int STRIDE, int MODE, int CHAIN>
-__device__ __forceinline__ int traverse4_chain(const DScene& S, const DNode4F* lds_nodes, const DPrim* lds_prims, v3& o,
-                                               v3& d, double t_min, double& t_best, int& face_best, unsigned* stk,
-                                               Rng& rng, uint64_t seed, int& depth_left, unsigned& chained,
-                                               unsigned& visits, unsigned& ptests) {
-  v3 inv;
-  RaySigns ns;
-  RayF rf;
-  Recip ra;
-  bool ra_ok;
-  float tmaxf;
-  int best, sp, node, steps;
-  unsigned top;
-  int budget = CHAIN;
-  auto begin = [&]() {
-    inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
-    ns = ray_signs(inv);
-    rf = ray_f<DNode4F>(S, o, inv);
-    const double a = len2(d);
-    ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_r)
-    ra_ok = a >= 0x1p-300 && a <= 0x1p300;
-    tmaxf = tmax_f32(t_best);
-    best = -1;
-    sp = 0;
-    top = ~0u;
-    node = S.root4;
-    steps = 0;
-  };
-  begin();
-  for (;;) {
-    if (steps < S.n_nodes4 && node >= 0) {  // (a tree traversal visits a node at most once: see traverse4)
-      node = visit4<STRIDE, MODE, false>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, ra, ra_ok, t_min, node, t_best,
-                                         tmaxf, best, face_best, sp, top, stk, rng, seed, visits, ptests);
-      ++steps;
-      continue;
-    }
-    if (budget == 0 || best < 0 || depth_left <= 1 || steps > RT_CHAIN_STEPS) break;
-    const DPrim pr = (MODE == kSceneLds) ? lds_prims[best] : S.prims[best];
-    if (!(pr.material & kPrimMatDielectric)) break;
-    // ray_color's loop body for this hit (render.rs:31-45): no emission, scatter, attenuation 1 (att
-    // unchanged, exactly), one more bounce of max_depth used
-    Hit h;
-    prim_record<false>(pr, face_best, o, d, t_best, h);
-    const DMat& m = S.mats[pr.material & kPrimMatMask];
-    const double ratio = h.front_face ? m.inv_param : m.param;  // 1.0 / ir, precomputed
-    const v3 ud = unit_fast(d);
-    const double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
-    const double sin_theta = sqrt_rn(1.0 - cos_theta * cos_theta);
-    bool refl = ratio * sin_theta > 1.0;
-    if (!refl) refl = reflectance_inl(cos_theta, ratio) > rng_next(rng, seed);  // drawn only if not TIR
-    o = h.point;
-    d = refl ? reflect(ud, h.normal) : refract(ud, h.normal, ratio);
-    --depth_left;
-    --budget;
-    ++chained;
-    t_best = __builtin_inf();
-    face_best = -1;
-    begin();
   }
   return best;
 }
@@ -1603,7 +1516,6 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
   const bool cam = kind == kDrawCam;
   const bool even = (r.draw & 1u) == 0u;
   uint64_t a0 = 0, a1 = 0, b0 = 0, b1 = 0;
-#ifndef RT_DONOR_BLOCKS
   if (cam || ((kind == kDrawSphere || kind == kDrawDiel) && even)) {
     PH_COUNT(12);
     philox_block(seed, r.pixel, r.sample, cam ? 0u : (r.draw >> 1), a0, a1);
@@ -1612,58 +1524,6 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
     PH_COUNT(13);
     philox_block(seed, r.pixel, r.sample, cam ? 1u : (r.draw >> 1) + 1u, b0, b1);
   }
-#else
-  // RT_DONOR_BLOCKS (measured ±0 on the headline, gen_spheres -2.8 %: DESIGN.md §5; compiled out).
-  // One Philox call site for the wave: every lane evaluates one block — its block A if it needs one,
-  // else its block B.  A lane that needs both (a new sample with a lens, a sphere attempt at an even
-  // draw) gets its block B from a lane that needs none (sky, a dielectric at an odd draw, idle): the
-  // j-th such lane evaluates it for the j-th needing lane.  Needing lanes beyond the donors evaluate
-  // their block B at a second call site, which the wave skips when every lane was served.
-  const bool need_a = cam || ((kind == kDrawSphere || kind == kDrawDiel) && even);
-  const bool need_b = kind == kDrawSphere || (cam && lens);
-  const uint32_t cb = cam ? 1u : (r.draw >> 1) + 1u;
-  const bool both = need_a && need_b, idle = !need_a && !need_b;
-  const unsigned long long E = __ballot(both), D = __ballot(idle);
-  const int nE = __popcll(E), nD = __popcll(D);
-  const int rk = __popcll((both ? E : D) & lanes_below());  // rank among its kind (both / idle lanes)
-  uint32_t pix = r.pixel, smp = r.sample, c = need_a ? (cam ? 0u : (r.draw >> 1)) : cb;
-  int partner = 0;
-  bool donor = false;
-  if (E != 0ull) {  // wave-uniform
-    const int pD = __shfl(rank_owners(D), rk), pE = __shfl(rank_owners(E), rk);
-    partner = both ? pD : pE;
-    donor = idle && rk < nE;
-    const uint32_t opix = (uint32_t)__shfl((int)r.pixel, partner), osmp = (uint32_t)__shfl((int)r.sample, partner);
-    const uint32_t oc = (uint32_t)__shfl((int)cb, partner);
-    if (donor) {
-      pix = opix;
-      smp = osmp;
-      c = oc;
-    }
-  }
-  PH_COUNT(12);
-  uint64_t e0, e1;
-  philox_block(seed, pix, smp, c, e0, e1);
-  if (need_a) {
-    a0 = e0;
-    a1 = e1;
-  } else {
-    b0 = e0;
-    b1 = e1;
-  }
-  if (E != 0ull) {  // wave-uniform
-    const uint64_t g0 = (uint64_t)__shfl((long long)e0, partner), g1 = (uint64_t)__shfl((long long)e1, partner);
-    if (both) {
-      if (rk < nD) {
-        b0 = g0;
-        b1 = g1;
-      } else {
-        PH_COUNT(13);
-        philox_block(seed, r.pixel, r.sample, cb, b0, b1);
-      }
-    }
-  }
-#endif
   const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
   // the first attempts' uniforms, converted once for every kind: a sphere takes u0 u1 u2 (x y z), a
   // camera u0 u1 (jitter) and u2 u3 (disk), a dielectric u0
@@ -1771,6 +1631,7 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
 // CAM: a DCamera (reference) or a pointer-like to one (the megakernel's constant-address-space copy).
 typedef __attribute__((address_space(4))) const DCamera KCamera;
 typedef __attribute__((address_space(4))) const DWork KWork;
+typedef __attribute__((address_space(4))) const DScene KScene;
 template <class CAM>
 __device__ __forceinline__ void camera_ray_drawn(const CAM& C, double x, double y, v3 disk, v3& o, v3& d) {
   const double xp = x / (double)C.width;
@@ -1834,13 +1695,13 @@ __device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
 }
 
 // image_texture.rs:34-56: clamp, flip v, truncate, /255.
-__device__ __forceinline__ v3 image_texel(const DScene& S, const DTex& tx, double u, double v) {
-  const DImage im = S.images[tx.table];
+__device__ __forceinline__ v3 image_texel(const DTex& tx, double u, double v) {
+  const DTexImage im = tx.img;
   double uu = (u > 0.0) ? ((u < 1.0) ? u : 1.0) : 0.0;
   double vv = 1.0 - ((v > 0.0) ? ((v < 1.0) ? v : 1.0) : 0.0);
   uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
   uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
-  const uint8_t* px = S.texels + im.offset + ((size_t)iy * (size_t)im.width + ix) * 3;
+  const uint8_t* px = im.texels + ((size_t)iy * (size_t)im.width + ix) * 3;
   const double cs = 1.0 / 255.0;
   return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
 }
@@ -1876,7 +1737,7 @@ __device__ __forceinline__ v3 leaf_texture_value(const DScene& S, int leaf, doub
   if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);  // solid.rs:17-21
   if (tx.kind == RT_TEX_PERLIN) return V(pn, pn, pn);
   const UV uv = hit_uv(S.prims[prim], face, h);
-  return image_texel(S, tx, uv.u, uv.v);
+  return image_texel(tx, uv.u, uv.v);
 }
 
 // `lds_perlin`: the block's LDS copy of the Perlin tables, or null (tables read through L1/L2).
@@ -1891,7 +1752,7 @@ __device__ __forceinline__ v3 texture_value(const DScene& S, const DPerlin* lds_
     return V(n, n, n);
   }
   const UV uv = hit_uv(S.prims[prim], face, h);
-  return image_texel(S, tx, uv.u, uv.v);
+  return image_texel(tx, uv.u, uv.v);
 }
 
 // x^5 for x in [0, 4] as a double-double product (x^2 and x^4 carried with their FMA-exact
@@ -1910,11 +1771,17 @@ __device__ __forceinline__ double pow5(double x) {
 }
 
 // dielectric.rs:15-19 (Schlick); only ever compared against a uniform draw (dielectric.rs:41)
+__device__ __forceinline__ double reflectance_inl(double cosine, double ref_idx) {
+  double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
+  r0 = r0 * r0;
+  return r0 + (1.0 - r0) * pow5(1.0 - cosine);
+}
 __device__ __noinline__ double reflectance(double cosine, double ref_idx) { return reflectance_inl(cosine, ref_idx); }
 
 // skybox/mod.rs:5-25
 // skybox/mod.rs:18-25 given un = unit(d)
-__device__ __forceinline__ v3 sky_unit(const DScene& S, v3 un) {
+template <class SC>  // a DScene, or the megakernel's constant-address-space copy (KScene)
+__device__ __forceinline__ v3 sky_unit(const SC& S, v3 un) {
   if (S.sky == RT_SKY_ABOVE) {
     double t = 0.5 * (un.y + 1.0);
     return scale(V(1.0, 1.0, 1.0), 1.0 - t) + scale(V(0.5, 0.7, 1.0), t);

@@ -100,12 +100,8 @@ static_assert(sizeof(DExt) == 144, "DExt layout");
 struct alignas(16) DPrim {
   double p[6];       // sphere: cx cy cz r 1/r ; rect: d1_min d1_max d2_min d2_max offset ; box: min xyz max xyz
   int32_t kind;
-  int32_t material;  // material index (kPrimMatMask) | kPrimMatDielectric when that material is a dielectric
+  int32_t material;  // material index
 };
-// DPrim.material's flag: the megakernel chains dielectric segments inside its traversal loop
-// (traverse4_chain) and decides it from the primitive alone.
-constexpr int32_t kPrimMatDielectric = 1 << 30;
-constexpr int32_t kPrimMatMask = kPrimMatDielectric - 1;
 static_assert(sizeof(DPrim) == 64, "DPrim layout");
 
 struct alignas(16) DMat {
@@ -117,10 +113,19 @@ struct alignas(16) DMat {
 };
 static_assert(sizeof(DMat) == 48, "DMat layout");
 
+// An image texture's RGB8 texels (device) and size, held in its DTex record: the texel lookup needs
+// no scene-wide table (whose pointers the megakernel would otherwise keep in SGPRs across its loop).
+struct DTexImage {
+  const uint8_t* texels;
+  int32_t width, height;
+};
 struct alignas(16) DTex {
   int32_t kind;   // RT_TEX_*
   int32_t odd, even, table;
-  double color[3];
+  union {
+    double color[3];  // RT_TEX_SOLID
+    DTexImage img;    // RT_TEX_IMAGE
+  };
   double scale;
 };
 static_assert(sizeof(DTex) == 48, "DTex layout");
@@ -130,19 +135,12 @@ struct DPerlin {
   int32_t perm_x[256], perm_y[256], perm_z[256];
 };
 
-struct DImage {
-  int32_t width, height;
-  int64_t offset;  // byte offset of the RGB8 texels in the image pool
-};
-
 struct DScene {
   const DNode* nodes;      // node 0 = top node (child[0] = root, child[1] = empty)
   const DPrim* prims;
   const DMat* mats;
   const DTex* texs;
   const DPerlin* perlin;
-  const DImage* images;
-  const uint8_t* texels;
   int32_t n_nodes, n_prims;
   int32_t stack_depth;     // max stack entries a traversal can need
   int32_t n_lds_nodes;     // nodes [0, n_lds_nodes) are copied into LDS per block (BFS order: top levels)
@@ -204,7 +202,7 @@ struct DWork {
   int32_t ty0;                   // first tile row of the window (rt_render_scanlines)
   uint64_t seed;
   uint64_t n_units;              // n_tiles_rank * n_chunks * 64
-  // megakernel with RT_BLOCK_SEGMENTS: the (tile-major) unit space cut into n_segs contiguous segments
+  // megakernel: the (tile-major) unit space cut into n_segs contiguous segments
   // of seg_len units (a multiple of 64), one per block (XCD-major: the blocks of one XCD own adjacent
   // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
   // segment, then steal from the next segments that still hold units
@@ -218,6 +216,12 @@ struct DCounters {
   unsigned long long pad[12];
 };
 constexpr int kCounterSlots = 64;
+// instrumented build: DCounters.pad slots of the megakernel's phase clocks (PH_STAMP in trace.hip) and
+// traversal step statistics
+enum : int {
+  kPhRegen = 0, kPhTrav = 1, kPhShade = 2, kPhLaneSteps = 3, kPhWaveSteps = 4, kPhRecord = 5, kPhMarble = 6,
+  kPhDraws = 7, kPhCamera = 8, kPhTail = 9, kPhBuckets = 10
+};
 
 struct KParams {
   DScene scene;
@@ -231,6 +235,7 @@ struct KParams {
   // formed instead of being held in SGPRs across the whole loop (where it spills to VGPR lanes)
   uint64_t cam_const;
   uint64_t work_const;           // device copy of `work`, read the same way where a unit is taken
+  uint64_t scene_const;          // device copy of `scene`, read the same way where the sky is shaded
 };
 
 // ---- wavefront engine (wavefront.hip): path state of P slots as structure-of-arrays in HBM ----

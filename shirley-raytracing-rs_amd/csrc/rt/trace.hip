@@ -42,27 +42,14 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 // 4 waves per SIMD, 128 VGPRs).  HIP's second launch-bounds argument is the minimum waves per SIMD.
 // EXT: the scene has book-2 primitives; their code is compiled into separate
 // instances so that reference scenes keep the kernel's register allocation.
-// (tuning switches for A/B builds: minimum waves per SIMD of the 256-thread instances)
-#ifndef RT_NARROW_WAVES_EXT
-#define RT_NARROW_WAVES_EXT 4
+#ifndef RT_KSCENE
+#define RT_KSCENE 1
 #endif
-#ifndef RT_NARROW_WAVES
-#define RT_NARROW_WAVES 4
-#endif
-// Dielectric segments a lane may chain inside one traversal call (traverse4_chain; 0 = off), reference
-// scenes only (the EXT instances keep traverse4).  Off: measured slower at every setting.
-#ifndef RT_CHAIN_MAX
-#define RT_CHAIN_MAX 0
-#endif
-constexpr int kChainMax = RT_CHAIN_MAX;
-// Units taken from per-block segments of the unit space (stealing from other segments once the
-// block's is empty) instead of one global queue: a block's waves stay on neighbouring tiles.
-#ifndef RT_BLOCK_SEGMENTS
-#define RT_BLOCK_SEGMENTS 1
-#endif
+// Minimum waves per SIMD of the 256-thread instances (4 = 128 VGPRs: 3 and 5 measured slower).
+constexpr int kNarrowWaves = 4;
 
 template <int THREADS, int MODE, bool EXT>
-__global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : (EXT ? RT_NARROW_WAVES_EXT : RT_NARROW_WAVES))
+__global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : kNarrowWaves)
 void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
@@ -88,7 +75,8 @@ void trace_kernel(KParams P) {
   // wave-uniform window of unit indices
   unsigned long long w_next = 0, w_end = 0;
   bool exhausted = false;
-#if RT_BLOCK_SEGMENTS
+  // units are taken from per-block segments of the unit space (stealing from other segments once the
+  // block's is empty) when DWork.n_segs != 0, else from one global queue.
   // the block's segment, XCD-major: blocks are dealt round-robin to the 8 XCDs, so block b (on XCD
   // b % 8) owns segment (b % 8) * ceil(n / 8) + b / 8 — an XCD's blocks own adjacent segments
   uint32_t seg;
@@ -96,7 +84,6 @@ void trace_kernel(KParams P) {
     const uint32_t per_xcd = (W.n_segs + 7u) / 8u, s0 = (blockIdx.x % 8u) * per_xcd + blockIdx.x / 8u;
     seg = s0 < W.n_segs ? s0 : blockIdx.x % max(W.n_segs, 1u);
   }
-#endif
 
   // lane state
   // (kept lean: every loop-carried VGPR here competes with the 128-VGPR budget of 4 waves per SIMD)
@@ -109,10 +96,21 @@ void trace_kernel(KParams P) {
   Rng rng{0, 0, 0, 0, 0};
   unsigned long long n_seg = 0, n_samp = 0;  // wave-uniform (SGPRs): popcounts of ballots
   unsigned visits = 0, ptests = 0;           // per lane; flushed to the counters before 2^31
-  unsigned chained = 0;                      // per lane: segments chained inside traverse4_chain
 
 #ifdef RT_PHASE_TIMING
-  unsigned long long ph_regen = 0, ph_trav = 0, ph_shade = 0, ph_lane_steps = 0, ph_wave_steps = 0;
+  // wave-uniform clock stamps at wave-uniform points of the loop (SGPR sums): the iteration's time by
+  // phase (kPh* buckets), plus the traversal step statistics
+  unsigned long long ph_t[kPhBuckets] = {}, ph_last = clock64(), ph_lane_steps = 0, ph_wave_steps = 0;
+#define PH_STAMP(b)                               \
+  do {                                            \
+    const unsigned long long ph_now = clock64();  \
+    ph_t[b] += ph_now - ph_last;                  \
+    ph_last = ph_now;                             \
+  } while (0)
+#else
+#define PH_STAMP(b) \
+  do {              \
+  } while (0)
 #endif
 #ifdef RT_TIMELINE
   const unsigned wave_gid = blockIdx.x * (THREADS / kWave) + tid / kWave;
@@ -126,7 +124,6 @@ void trace_kernel(KParams P) {
   // (4) shading; ended lanes add their radiance and publish finished units; new samples' camera rays.
   for (;;) {
 #ifdef RT_PHASE_TIMING
-    const unsigned long long ph1 = clock64();
     const unsigned long long ph_before = ph_lane_steps;
 #endif
     // 1. one ray_color iteration (render.rs:30-46): closest hit and hit record, the material and the
@@ -139,31 +136,22 @@ void trace_kernel(KParams P) {
     h.normal = h.point;
     h.t = h.u = h.v = 0.0;
     h.front_face = false;
-#ifdef RT_PHASE_TIMING
-    unsigned long long ph2 = ph1;
-#endif
     PH_COUNT(6);
     n_seg += __popcll(__ballot(active));
     if (active) {
+      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
+                                      ptests RT_STAT_ARG(ph_lane_steps));
 #ifdef RT_PHASE_TIMING
-      prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits, ptests,
-                                      ph_lane_steps);
-      ph2 = clock64();
-      ph_trav += ph2 - ph1;
-#else
-      if constexpr (!EXT && kChainMax > 0)  // dielectric segments chained inside the traversal loop
-        prim = traverse4_chain<THREADS, MODE, kChainMax>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng,
-                                                         seed, depth_left, chained, visits, ptests);
-      else
-        prim = traverse4<THREADS, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
-                                        ptests);
+    }  // (instrumented build: the traversal's stamp at a wave-uniform point)
+    PH_STAMP(kPhTrav);
+    {
 #endif
       if (prim >= 0) {
         PH_COUNT(15);
         hit = true;
         const DPrim pr = (MODE == kSceneLds) ? lds_prims[prim] : S.prims[prim];  // (LDS copy when resident)
         hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
-        mat = pr.material & kPrimMatMask;
+        mat = pr.material;
         mk = S.mats[mat].kind;
         need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
         if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
@@ -177,9 +165,7 @@ void trace_kernel(KParams P) {
         }
       }
     }
-#ifdef RT_PHASE_TIMING
-    const unsigned long long ph0 = clock64();
-#endif
+    PH_STAMP(kPhRecord);
     // 2. the path ends at this segment when it misses (the sky) or meets a material that does not
     // scatter (diffuse light): known before shading, so the lane's next sample starts in this iteration
     const bool ends = active && (!hit || mk == RT_MAT_DIFFUSE_LIGHT);
@@ -204,7 +190,6 @@ void trace_kernel(KParams P) {
         idx = w_next + rank;
         w_next += k;
       } else {
-#if RT_BLOCK_SEGMENTS
         unsigned long long nb = W.n_units;
         if (W.n_segs != 0u) {
         // the block's segment (consecutive chunks of neighbouring tiles: coherent lanes, the same
@@ -245,14 +230,6 @@ void trace_kernel(KParams P) {
           nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
                (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
         }
-#else
-        unsigned long long nb = 0;
-        if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)kWave);
-        // the whole wave is here (the loop's control flow is uniform), so lane 0 is the first active
-        // lane; readfirstlane (not a shuffle) lets the compiler keep the window in SGPRs
-        nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
-             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
-#endif
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
         w_end = nb + kWave;
@@ -296,13 +273,11 @@ void trace_kernel(KParams P) {
       rng.sample += 1u;
       rng.draw = 0;
     }
-#ifdef RT_PHASE_TIMING
-    const unsigned long long ph3 = clock64();
-    ph_regen += ph3 - ph0;
-#endif
+    PH_STAMP(kPhRegen);
     // 3. Perlin marble values for the lanes that need one, by the whole wave (wave-uniform)
     const double pn = lds_perlin ? marble_coop((LdsPerlin*)lds_perlin, need_pn, ptab, psc, h.point)
                                  : marble_coop(S.perlin, need_pn, ptab, psc, h.point);
+    PH_STAMP(kPhMarble);
     // every draw of the iteration, by the wave: the scatter's random_in_unit_sphere, the dielectric's
     // uniform, a new sample's jitter and lens point
     const bool scat = active && !ends;
@@ -313,6 +288,7 @@ void trace_kernel(KParams P) {
     // the one normalisation a lane's shading needs, for all lanes at once: unit(r) for a lambertian /
     // fairy light scatter, unit(d) for dielectric, metal and the sky (others: a dummy)
     const v3 un = unit_fast(!active ? V(1.0, 1.0, 1.0) : (scat && need_r && mk != RT_MAT_METAL) ? rs : d);
+    PH_STAMP(kPhDraws);
     // 4. emitted + scatter (render.rs:31-45) or the sky; an ended lane's o, d are free once un holds
     // unit(d), so its new sample's camera ray is formed first
     if (regen) {
@@ -323,6 +299,7 @@ void trace_kernel(KParams P) {
       asm volatile("" : "+s"(kc));
       camera_ray_drawn(*kc, jx, jy, rs, o, d);
     }
+    PH_STAMP(kPhCamera);
     if (active) {
       bool alive, has_emit = false;
       v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
@@ -331,7 +308,15 @@ void trace_kernel(KParams P) {
         alive = shade_factor(S, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
       } else {
         PH_COUNT(20);
+#if RT_KSCENE
+        // the sky's kind and colour read with scalar loads here, like the camera (held in SGPRs across
+        // the loop they spill to VGPR lanes)
+        KScene* ks = (KScene*)(uintptr_t)P.scene_const;
+        asm volatile("" : "+s"(ks));
+        emit = sky_unit(*ks, un);
+#else
         emit = sky_unit(S, un);
+#endif
         has_emit = true;
         alive = false;
       }
@@ -344,6 +329,7 @@ void trace_kernel(KParams P) {
         active = false;
       }
     }
+    PH_STAMP(kPhShade);
     // a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
     if (publish) {
       PH_COUNT(24);
@@ -359,9 +345,7 @@ void trace_kernel(KParams P) {
       depth_left = W.max_depth;  // >= 1: max_depth == 0 frames are written by render_window itself
       active = true;
     }
-#ifdef RT_PHASE_TIMING
-    ph_shade += clock64() - ph3;
-#endif
+    PH_STAMP(kPhTail);
 #ifdef RT_TIMELINE
     if (exhausted && !ph_exh_seen) {
       ph_exh_seen = true;
@@ -371,7 +355,7 @@ void trace_kernel(KParams P) {
     // done when no lane holds a path or a unit and the pool is drained (a lane that fails to get a
     // unit while the pool is not drained — e.g. an edge tile's unit outside the image — retries)
     if (exhausted && !__any(active || has_unit)) break;
-#ifdef RT_PHASE_TIMING
+#if defined(RT_PHASE_TIMING) && !defined(RT_PHASE_NO_EVENTS)
     {
       unsigned dl = (unsigned)(ph_lane_steps - ph_before);  // this lane's steps (0 when idle)
       if (dl > 0) atomicAdd(&g_visit_hist[min(dl, 63u)], 1ull);
@@ -391,27 +375,25 @@ void trace_kernel(KParams P) {
   if (lane == 0 && wave_gid < (unsigned)kTimelineWaves) g_wave_t1[wave_gid] = __builtin_amdgcn_s_memrealtime();
 #endif
   // wave-reduce the per-lane counters, one atomic per wave
-  unsigned long long n_vis = visits, n_pt = ptests, n_ch = chained;
+  unsigned long long n_vis = visits, n_pt = ptests;
   for (int off = 32; off > 0; off >>= 1) {
     n_vis += __shfl_down(n_vis, off);
     n_pt += __shfl_down(n_pt, off);
-    n_ch += __shfl_down(n_ch, off);
   }
 #ifdef RT_PHASE_TIMING
   for (int off = 32; off > 0; off >>= 1) ph_lane_steps += __shfl_down(ph_lane_steps, off);
-  if (lane == 0) atomicAdd(&P.counters[blockIdx.x % kCounterSlots].pad[3], ph_lane_steps);
+  if (lane == 0) atomicAdd(&P.counters[blockIdx.x % kCounterSlots].pad[kPhLaneSteps], ph_lane_steps);
 #endif
   if (lane == 0) {
     DCounters* cs = P.counters + (blockIdx.x % kCounterSlots);
-    atomicAdd(&cs->segments, n_seg + n_ch);
+    atomicAdd(&cs->segments, n_seg);
     atomicAdd(&cs->samples, n_samp);
     atomicAdd(&cs->node_visits, n_vis);
     atomicAdd(&cs->prim_tests, n_pt);
 #ifdef RT_PHASE_TIMING
-    atomicAdd(&cs->pad[0], ph_regen);
-    atomicAdd(&cs->pad[1], ph_trav);
-    atomicAdd(&cs->pad[2], ph_shade);
-    atomicAdd(&cs->pad[4], ph_wave_steps);
+    for (int b = 0; b < kPhBuckets; ++b)
+      if (b != kPhLaneSteps && b != kPhWaveSteps) atomicAdd(&cs->pad[b], ph_t[b]);
+    atomicAdd(&cs->pad[kPhWaveSteps], ph_wave_steps);
 #endif
   }
 }
@@ -572,12 +554,9 @@ __global__ __launch_bounds__(kHitThreads) void hit4_kernel(DScene S, const doubl
   const Rng rk{(uint32_t)i, 0u, 0u, 0u, 0u};  // side-stream key of a free ray, as hit_kernel's
 #ifdef RT_PHASE_TIMING
   unsigned long long steps = 0;
-  const int prim = traverse4<kHitThreads, MODE, EXT>(S, lds_nodes, lds_prims, o, d, t_min, t_best, face, stk, rk, 0ull,
-                                                      visits, ptests, steps);
-#else
-  const int prim = traverse4<kHitThreads, MODE, EXT>(S, lds_nodes, lds_prims, o, d, t_min, t_best, face, stk, rk, 0ull,
-                                                      visits, ptests);
 #endif
+  const int prim = traverse4<kHitThreads, MODE, EXT>(S, lds_nodes, lds_prims, o, d, t_min, t_best, face, stk, rk, 0ull,
+                                                      visits, ptests RT_STAT_ARG(steps));
   HitOut r{};
   r.object = prim;
   if (prim >= 0) {

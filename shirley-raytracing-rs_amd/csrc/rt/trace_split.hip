@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kTraceThreadsWide, 1) void split_kernel(KParams P) 
         hit = true;
         const DPrim pr = S.prims[prim];
         hit_record<false, false>(S, pr, face, o, d, t_best, rng, seed, h);
-        mat = pr.material & kPrimMatMask;
+        mat = pr.material;
         mk = S.mats[mat].kind;
         need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
         if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {

@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
       Hit h;
       hit_record<false, EXT>(S, pr, face, o, d, t, rng, seed, h);
       hp = h.point;
-      const DMat m = S.mats[pr.material & kPrimMatMask];
+      const DMat m = S.mats[pr.material];
       if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
         double ratio = h.front_face ? (1.0 / m.param) : m.param;
         v3 ud = unit(d);
@@ -308,7 +308,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
             a = V(tx.color[0], tx.color[1], tx.color[2]);
           } else {
             const UV uv = hit_uv(pr, face, h);
-            a = image_texel(S, tx, uv.u, uv.v);
+            a = image_texel(tx, uv.u, uv.v);
           }
         }
         if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters

@@ -81,3 +81,52 @@ def test_mislabelled_runs_exit_nonzero():
     assert r.returncode != 0 and "visible GPU" in r.stderr
     r = _run(["--gpus", "2", "--rank-env-only"], {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_multi_rank_check_comparison():
+    """bench.py's multi_rank_check verdicts: tiles bit for bit, samples within 1e-12
+    relative; shape changes, single-ulp flips in the tile frame, NaNs and reassociation-sized errors."""
+    import numpy as np
+    b = _bench()
+    rng = np.random.default_rng(7)
+    ref = rng.random((112, 200, 3)) * 8.0
+    ok, detail = b.compare_frames(ref, ref.copy(), exact=True)
+    assert ok and "bit-identical" in detail
+    one_ulp = ref.copy()
+    one_ulp[5, 7, 1] = np.nextafter(one_ulp[5, 7, 1], np.inf)
+    ok, detail = b.compare_frames(ref, one_ulp, exact=True)
+    assert not ok and detail.startswith("1 of")
+    ok, _ = b.compare_frames(ref, one_ulp, exact=False)  # one ulp is within the reassociation bound
+    assert ok
+    far = ref.copy()
+    far[0, 0, 0] *= 1.0 + 1e-9
+    ok, detail = b.compare_frames(ref, far, exact=False)
+    assert not ok and "beyond" in detail
+    nan = ref.copy()
+    nan[3, 3, 2] = np.nan
+    assert not b.compare_frames(ref, nan, exact=False)[0]
+    assert not b.compare_frames(ref, nan, exact=True)[0]
+    zero = np.zeros_like(ref)
+    assert b.compare_frames(zero, zero.copy(), exact=False)[0]
+    assert not b.compare_frames(ref, ref[:100], exact=True)[0]
+
+
+def test_resolve_partition():
+    b = _bench()
+    assert b.resolve_partition("tiles", {}) == "tiles"
+    assert b.resolve_partition("samples", {}) == "samples"
+    assert b.resolve_partition("auto", {}) == "tiles"
+    assert b.resolve_partition("auto", {"SHIRLEY_PARTITION": "samples"}) == "samples"
+
+
+def test_cpu_leg_sizes_the_frame_to_the_time_budget():
+    """bench.py's per-config CPU legs (configs 3-5, BASELINE.md:24,33-35): the oracle over the full frame
+    at an spp sized to the time budget, never above the config's own spp."""
+    import oracle_lib as O
+    from raytracer import SceneBuilder, scene_camera
+    b = _bench()
+    args = argparse.Namespace(max_depth=50, seed=0x5EED)
+    desc = SceneBuilder.builtin("cornell", 0x5EED).finalize(0x5EED)
+    cam = scene_camera("cornell", 48, "square")
+    n, dt, spp = b.cpu_leg(O.OracleScene(desc), cam, 4, args, 2, 0.2, O)
+    assert 1 <= spp <= 4 and n == cam.image_width * cam.image_height * spp and dt > 0

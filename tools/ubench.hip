@@ -17,6 +17,9 @@ __global__ __launch_bounds__(1024) void kern(int n, unsigned long long* out, uns
     w[i] = a[i];
   }
   unsigned k = 0xD2511F53u;
+  unsigned long long sm = 0x5555aaaa3333ccccull ^ (unsigned long long)n;
+  unsigned long long cm[CHAINS];
+  for (int i = 0; i < CHAINS; ++i) cm[i] = sm >> i;
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
   for (int it = 0; it < n; ++it) {
 #pragma unroll
@@ -43,10 +46,26 @@ __global__ __launch_bounds__(1024) void kern(int n, unsigned long long* out, uns
       if (OP == 19) asm volatile("v_mad_u32_u24 %0, %0, %1, %0" : "+v"(a[i]) : "s"(k));
       if (OP == 20) asm volatile("v_mul_f64 %0, %0, %0" : "+v"(f[i]));
       if (OP == 21) asm volatile("v_cvt_f32_f64 %0, %1" : "=v"(a[i]) : "v"(f[i]));
+      if (OP == 22) asm volatile("v_mov_b64 %0, %1" : "=v"(w[i]) : "v"(f[(i + 1) % CHAINS]));
+      if (OP == 23) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]), "s"(k));
+      if (OP == 24) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]), "s"(k));
+      if (OP == 25) asm volatile("v_add_u32 %0, %0, %1" : "+v"(a[i]) : "s"(k));
+      if (OP == 26) asm volatile("v_mov_b32_dpp %0, %1 row_shr:1" : "=v"(a[i]) : "v"(a[(i + 1) % CHAINS]));
+      if (OP == 27) asm volatile("v_cndmask_b32 %0, %0, %1, vcc\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]));
+      if (OP == 28) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]), "s"(k));
+      if (OP == 29) asm volatile("v_lshl_add_u64 %0, %0, 3, %1" : "+v"(w[i]) : "v"(w[(i + 1) % CHAINS]));
+      if (OP == 30) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(k), "s"(sm));
+      if (OP == 31) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(k) : );
+      if (OP == 32) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]), "s"(sm));
+      if (OP == 33) asm volatile("v_cmp_lt_u32 %0, %1, %2" : "=s"(cm[i]) : "v"(a[i]), "v"(k));
+      if (OP == 34) asm volatile("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(k) : "vcc");
+      if (OP == 35) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(k), "s"(cm[i]));
+      if (OP == 36) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]));
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   unsigned s = 0;
+  for (int i = 0; i < CHAINS; ++i) s ^= (unsigned)cm[i];
   for (int i = 0; i < CHAINS; ++i) s ^= a[i] ^ (unsigned)w[i] ^ (unsigned)(w[i] >> 32) ^ (unsigned)__double_as_longlong(f[i]);
   if (s == 0x12345678u) sink[0] = s;
   if (threadIdx.x % 64 == 0) out[blockIdx.x * 12 + threadIdx.x / 64] = t1 - t0;
@@ -81,8 +100,11 @@ int main(int argc, char** argv) {
                          "v_fma_f64", "v_add_f64", "v_rcp_f64", "v_sqrt_f64", "v_fma_f32", "v_pk_fma_f32",
                          "v_div_scale_f64", "v_cndmask_b32", "v_cvt_f64_u32", "v_ldexp_f64", "v_readlane_b32",
                          "v_min_f64", "v_cmp_lt_f64", "ds_bpermute+wait", "v_mad_u32_u24", "v_mul_f64",
-                         "v_cvt_f32_f64"};
-  double c[22];
+                         "v_cvt_f32_f64", "v_mov_b64", "v_bitop3_b32", "v_perm_b32", "v_add_u32", "v_mov_b32_dpp",
+                         "2x v_cndmask_b32", "v_max3_f32", "v_lshl_add_u64", "cndmask_e64 s-mask", "cndmask vcc const",
+                         "cndmask_e64 s nb", "v_cmp_lt_u32 ->s", "cmp+cndmask vcc", "cndmask_e64 cm", "v_max_u32 nb"};
+  const int nops = 37;
+  double c[37];
   c[0] = run<0>(n, blocks, d, sink); c[1] = run<1>(n, blocks, d, sink); c[2] = run<2>(n, blocks, d, sink);
   c[3] = run<3>(n, blocks, d, sink); c[4] = run<4>(n, blocks, d, sink); c[5] = run<5>(n, blocks, d, sink);
   c[6] = run<6>(n, blocks, d, sink); c[7] = run<7>(n, blocks, d, sink); c[8] = run<8>(n, blocks, d, sink);
@@ -90,8 +112,13 @@ int main(int argc, char** argv) {
   c[12] = run<12>(n, blocks, d, sink); c[13] = run<13>(n, blocks, d, sink); c[14] = run<14>(n, blocks, d, sink);
   c[15] = run<15>(n, blocks, d, sink); c[16] = run<16>(n, blocks, d, sink); c[17] = run<17>(n, blocks, d, sink);
   c[18] = run<18>(n, blocks, d, sink); c[19] = run<19>(n, blocks, d, sink); c[20] = run<20>(n, blocks, d, sink);
-  c[21] = run<21>(n, blocks, d, sink);
+  c[21] = run<21>(n, blocks, d, sink); c[22] = run<22>(n, blocks, d, sink); c[23] = run<23>(n, blocks, d, sink);
+  c[24] = run<24>(n, blocks, d, sink); c[25] = run<25>(n, blocks, d, sink); c[26] = run<26>(n, blocks, d, sink);
+  c[27] = run<27>(n, blocks, d, sink); c[28] = run<28>(n, blocks, d, sink); c[29] = run<29>(n, blocks, d, sink);
+  c[30] = run<30>(n, blocks, d, sink); c[31] = run<31>(n, blocks, d, sink); c[32] = run<32>(n, blocks, d, sink);
+  c[33] = run<33>(n, blocks, d, sink); c[34] = run<34>(n, blocks, d, sink); c[35] = run<35>(n, blocks, d, sink);
+  c[36] = run<36>(n, blocks, d, sink);
   printf("threads/block %d (%d waves per SIMD): SIMD cycles per wave-instruction\n", g_threads, g_threads / 256);
-  for (int i = 0; i < 22; ++i) printf("%-18s %6.2f\n", names[i], c[i]);
+  for (int i = 0; i < nops; ++i) printf("%-18s %6.2f\n", names[i], c[i]);
   return 0;
 }
