@@ -238,17 +238,22 @@ int render_scene(const Args& a, const rt_scene_desc* desc, const rt_camera& cam)
     int done = 0;
     if (!a.resume.empty()) {
       Checkpoint ck;
-      std::ifstream f(a.resume, std::ios::binary);
-      f.read((char*)accum.data(), (std::streamsize)(n * sizeof(double)));
-      if (!read_checkpoint(a.resume, &ck) || !f || f.gcount() != (std::streamsize)(n * sizeof(double)) ||
-          f.peek() != std::char_traits<char>::eof()) {
-        std::fprintf(stderr, "error: %s is not a checkpoint of this frame size\n", a.resume.c_str());
+      if (!read_checkpoint(a.resume, &ck)) {
+        std::fprintf(stderr, "error: %s.json is not a checkpoint record\n", a.resume.c_str());
         rt_destroy(ctx);
         return 1;
       }
       const std::string why = checkpoint_mismatch(ck, checkpoint_of(a, desc, cam, samples, 0));
       if (!why.empty()) {
         std::fprintf(stderr, "error: %s is a checkpoint of another frame: %s\n", a.resume.c_str(), why.c_str());
+        rt_destroy(ctx);
+        return 1;
+      }
+      std::ifstream f(a.resume, std::ios::binary);
+      f.read((char*)accum.data(), (std::streamsize)(n * sizeof(double)));
+      if (!f || f.gcount() != (std::streamsize)(n * sizeof(double)) || f.peek() != std::char_traits<char>::eof()) {
+        std::fprintf(stderr, "error: %s does not hold the %zu sums of a %dx%d frame\n", a.resume.c_str(), n,
+                     cam.image_width, cam.image_height);
         rt_destroy(ctx);
         return 1;
       }

@@ -642,6 +642,10 @@ DCamera device_camera(const rt_camera* c) {
   d.height = c->image_height;
   d.has_lens = c->has_lens;
   d.lens_radius = c->lens_radius;
+  d.wd = (double)c->image_width;
+  d.hd = (double)c->image_height;
+  d.inv_w = 1.0 / d.wd;  // correctly rounded (IEEE division)
+  d.inv_h = 1.0 / d.hd;
   for (int k = 0; k < 3; ++k) {
     d.origin[k] = c->origin[k];
     d.u[k] = c->u[k];

@@ -81,6 +81,17 @@ __device__ __forceinline__ v3 unit_fast(v3 a) {
   }
   return V(a.x / n, a.y / n, a.z / n);
 }
+// 1.0 / d per component, bit-identical to the IEEE division (aabb.rs:66 `1.0 / r.direction[a]`): with
+// every |d_i| in [2^-300, 2^300] the compiler's own division sequence reduces to div_recip(1, recip(d_i))
+// (see Recip; checked on the GPU by tools/divcheck.hip), 7 instructions instead of 11; one range test
+// for the three components, the division itself otherwise (0, inf, NaN, extreme magnitudes).
+__device__ __forceinline__ v3 inv_dir(v3 d) {
+  const double lo = fmin(fmin(fabs(d.x), fabs(d.y)), fabs(d.z));
+  const double hi = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
+  if (lo >= 0x1p-300 && hi <= 0x1p300)
+    return V(div_recip(1.0, recip(d.x)), div_recip(1.0, recip(d.y)), div_recip(1.0, recip(d.z)));
+  return V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+}
 __device__ __forceinline__ double comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 // vec3.rs:129-132
 __device__ __forceinline__ bool near_zero(v3 a) {
@@ -1148,7 +1159,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
 #endif
                                          ) {
   PH_COUNT(23);
-  const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  const v3 inv = inv_dir(d);
   const RaySigns ns = ray_signs(inv);
   const RayF rf = ray_f<typename Node4Sel<EXT>::T>(S, o, inv);
   const double a = len2(d);
@@ -1186,7 +1197,7 @@ struct Trav4 {
 
 template <bool EXT>
 __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 d, double t_max) {
-  T.inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  T.inv = inv_dir(d);
   T.ns = ray_signs(T.inv);
   T.rf = ray_f<typename Node4Sel<EXT>::T>(S, o, T.inv);
   T.ra = recip(len2(d));
@@ -1409,7 +1420,21 @@ __device__ __forceinline__ void philox_block(uint64_t seed, uint32_t pixel, uint
   even = (uint64_t)c0 | ((uint64_t)c1 << 32);
   odd = (uint64_t)c2 | ((uint64_t)c3 << 32);
 }
-__device__ __forceinline__ double unit_draw(uint64_t v) { return (double)(v >> 11) * (1.0 / 9007199254740992.0); }
+// A draw's 53 random bits, v >> 11 (< 2^53), as an exact double: the high 21 bits times 2^32 plus the
+// low 32 bits in one FMA (every term exact).  rand 0.8's Standard f64 is draw_bits(v) * 2^-53.
+__device__ __forceinline__ double draw_bits(uint64_t v) {
+  const uint64_t m = v >> 11;
+  return fma((double)(uint32_t)(m >> 32), 4294967296.0, (double)(uint32_t)m);
+}
+__device__ __forceinline__ double unit_draw(uint64_t v) { return __builtin_amdgcn_ldexp(draw_bits(v), -53); }
+// a + s * gen::<f64>() for s = 2^k (core/math.rs:22-25 random_real(-1, 1): a = -1, s = 2; the camera jitter
+// i + U, render.rs:60-63: a = i, s = 1): s * U is exact, so the reference rounds once, at the sum — the
+// single rounding of one FMA on the exact draw bits (2^(k-53) scales them exactly).
+__device__ __forceinline__ double affine_draw(uint64_t v, double pow2_over_2_53, double a) {
+  return fma(draw_bits(v), pow2_over_2_53, a);
+}
+constexpr double kTwoOver2p53 = 0x1p-52;  // random_real(-1, 1): (1 - -1) * 2^-53
+constexpr double kOneOver2p53 = 0x1p-53;
 
 // core/math.rs:32-45 random_in_unit_sphere for every lane with `need`, by the whole wave.  Each such
 // lane first makes its own attempt (the serial loop's first iteration, 52 % accepted).  The lanes it
@@ -1432,9 +1457,9 @@ __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, 
     if (!odd) philox_block(seed, r.pixel, r.sample, r.draw >> 1, a0, a1);
     philox_block(seed, r.pixel, r.sample, (r.draw >> 1) + 1u, b0, b1);
     const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
-    const double x = -1.0 + (1.0 - -1.0) * unit_draw(odd ? cached : a0);  // random_real(-1, 1), same ops
-    const double y = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b0 : a1);
-    const double z = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b1 : b0);
+    const double x = affine_draw(odd ? cached : a0, kTwoOver2p53, -1.0);  // random_real(-1, 1)
+    const double y = affine_draw(odd ? b0 : a1, kTwoOver2p53, -1.0);
+    const double z = affine_draw(odd ? b1 : b0, kTwoOver2p53, -1.0);
     r.draw += 3u;
     r.c2 = (uint32_t)b1;  // the odd half of block d/2 + 1, as the serial draws leave it
     r.c3 = (uint32_t)(b1 >> 32);
@@ -1456,9 +1481,9 @@ __device__ __forceinline__ v3 random_in_unit_sphere_coop(Rng& r, uint64_t seed, 
     philox_block(seed, pix, smp, t >> 1, a0, a1);
     philox_block(seed, pix, smp, (t >> 1) + 1u, b0, b1);
     const bool odd = (t & 1u) != 0u;
-    const double x = -1.0 + (1.0 - -1.0) * unit_draw(odd ? a1 : a0);  // random_real(-1, 1), same ops
-    const double y = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b0 : a1);
-    const double z = -1.0 + (1.0 - -1.0) * unit_draw(odd ? b1 : b0);
+    const double x = affine_draw(odd ? a1 : a0, kTwoOver2p53, -1.0);  // random_real(-1, 1)
+    const double y = affine_draw(odd ? b0 : a1, kTwoOver2p53, -1.0);
+    const double z = affine_draw(odd ? b1 : b0, kTwoOver2p53, -1.0);
     const unsigned long long acc = __ballot(len2(V(x, y, z)) <= 1.0);
     // owners' first accepted attempt, level by level (wave-uniform masks of n bits)
     const unsigned long long owners = (n == 64) ? ~0ull : ((1ull << n) - 1ull);
@@ -1525,29 +1550,29 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
     philox_block(seed, r.pixel, r.sample, cam ? 1u : (r.draw >> 1) + 1u, b0, b1);
   }
   const uint64_t cached = (uint64_t)r.c2 | ((uint64_t)r.c3 << 32);
-  // the first attempts' uniforms, converted once for every kind: a sphere takes u0 u1 u2 (x y z), a
-  // camera u0 u1 (jitter) and u2 u3 (disk), a dielectric u0
+  // the first attempts' draw bits, converted once for every kind: a sphere takes u0 u1 u2 (x y z), a
+  // camera u0 u1 (jitter) and u2 u3 (disk), a dielectric u0; each kind then scales them (affine_draw)
   const bool sph = kind == kDrawSphere;
-  const double u0 = unit_draw((!even && !cam) ? cached : a0);
-  const double u1 = unit_draw((sph && !even) ? b0 : a1);
-  const double u2 = unit_draw((sph && !even) ? b1 : b0);
-  const double u3 = unit_draw(b1);
+  const double u0 = draw_bits((!even && !cam) ? cached : a0);
+  const double u1 = draw_bits((sph && !even) ? b0 : a1);
+  const double u2 = draw_bits((sph && !even) ? b1 : b0);
+  const double u3 = draw_bits(b1);
   v3 p = V(0.0, 0.0, 0.0);
   bool pending = false;
   if (sph) {
-    p = V(-1.0 + (1.0 - -1.0) * u0, -1.0 + (1.0 - -1.0) * u1, -1.0 + (1.0 - -1.0) * u2);  // random_real(-1, 1)
+    p = V(fma(u0, kTwoOver2p53, -1.0), fma(u1, kTwoOver2p53, -1.0), fma(u2, kTwoOver2p53, -1.0));  // random_real(-1, 1)
     r.draw += 3u;
     r.c2 = (uint32_t)b1;  // the odd half of block d/2 + 1, as the serial draws leave it
     r.c3 = (uint32_t)(b1 >> 32);
     pending = !(len2(p) <= 1.0);
   } else if (kind == kDrawDiel) {
-    p = V(u0, u64_as_double(even ? a1 : cached), 0.0);
+    p = V(__builtin_amdgcn_ldexp(u0, -53), u64_as_double(even ? a1 : cached), 0.0);
   } else if (cam) {
-    jx = (double)(pxy & 0xffffu) + u0;
-    jy = (double)(pxy >> 16) + u1;
+    jx = fma(u0, kOneOver2p53, (double)(pxy & 0xffffu));  // i + U (render.rs:60-63)
+    jy = fma(u1, kOneOver2p53, (double)(pxy >> 16));
     r.draw = 2u;
     if (lens) {
-      const double x = -1.0 + (1.0 - -1.0) * u2, y = -1.0 + (1.0 - -1.0) * u3;
+      const double x = fma(u2, kTwoOver2p53, -1.0), y = fma(u3, kTwoOver2p53, -1.0);
       p = V(x, y, 0.0);
       r.draw = 4u;
       pending = !(x * x + y * y <= 1.0);  // len2((x, y, 0)): the + 0*0 term cannot change a sum >= 0
@@ -1582,8 +1607,8 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
     uint64_t e0, e1, f0, f1;
     philox_block(seed, pix, smp, c, e0, e1);
     philox_block(seed, pix, smp, c + 1u, f0, f1);
-    const double d0 = -1.0 + (1.0 - -1.0) * unit_draw(e0), d1 = -1.0 + (1.0 - -1.0) * unit_draw(e1);
-    const double d2 = -1.0 + (1.0 - -1.0) * unit_draw(f0), d3 = -1.0 + (1.0 - -1.0) * unit_draw(f1);
+    const double d0 = affine_draw(e0, kTwoOver2p53, -1.0), d1 = affine_draw(e1, kTwoOver2p53, -1.0);
+    const double d2 = affine_draw(f0, kTwoOver2p53, -1.0), d3 = affine_draw(f1, kTwoOver2p53, -1.0);
     double x, y, z;
     bool acc;
     uint32_t used;  // draws this item consumed up to its accepted point (disk)
@@ -1632,10 +1657,21 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
 typedef __attribute__((address_space(4))) const DCamera KCamera;
 typedef __attribute__((address_space(4))) const DWork KWork;
 typedef __attribute__((address_space(4))) const DScene KScene;
+// x / n for the camera's jittered pixel coordinate x in [0, n], n = width or height <= 65536, with
+// r = RN(1 / n) from the host: q0 = x r is within an ulp of x / n, and one correction step with the
+// correctly rounded reciprocal gives the correctly rounded quotient (Markstein, IBM J. Res. Dev. 34,
+// 1990) — bit-identical to the IEEE division the reference does (camera/mod.rs:98-99), at a mul and two
+// fmas instead of the ~11-instruction division.  Checked on the CPU against x / n for every n <= 4096
+// and every 97th n up to 65536, ~76 M jittered coordinates with edge cases (tools/camdiv_check.c,
+// tests/test_divisions.py), and on the GPU by every parity test (same bits as the oracle's x / n).
+__device__ __forceinline__ double pixel_coord_div(double x, double n, double r) {
+  const double q0 = x * r;
+  return __builtin_fma(__builtin_fma(-n, q0, x), r, q0);
+}
 template <class CAM>
 __device__ __forceinline__ void camera_ray_drawn(const CAM& C, double x, double y, v3 disk, v3& o, v3& d) {
-  const double xp = x / (double)C.width;
-  const double yp = y / (double)C.height;
+  const double xp = pixel_coord_div(x, C.wd, C.inv_w);
+  const double yp = pixel_coord_div(y, C.hd, C.inv_h);
   const v3 u = V(C.u[0], C.u[1], C.u[2]), v = V(C.v[0], C.v[1], C.v[2]);
   const v3 origin = V(C.origin[0], C.origin[1], C.origin[2]);
   v3 offset = V(0.0, 0.0, 0.0);
@@ -1988,8 +2024,8 @@ __device__ __forceinline__ bool shade_factor(const DScene& S, const DMat& m, int
 // camera/mod.rs:97-132 (horizontal / vertical / lower_left precomputed on the host, same ops)
 __device__ __forceinline__ void camera_ray(const DCamera& C, Rng& rng, uint64_t seed, double x, double y, v3& o,
                                            v3& d) {
-  double xp = x / (double)C.width;
-  double yp = y / (double)C.height;
+  double xp = pixel_coord_div(x, C.wd, C.inv_w);
+  double yp = pixel_coord_div(y, C.hd, C.inv_h);
   v3 u = V(C.u[0], C.u[1], C.u[2]), v = V(C.v[0], C.v[1], C.v[2]);
   v3 origin = V(C.origin[0], C.origin[1], C.origin[2]);
   v3 offset = V(0.0, 0.0, 0.0);

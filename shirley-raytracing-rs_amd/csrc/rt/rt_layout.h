@@ -170,6 +170,9 @@ struct DCamera {
   double lens_radius;
   double origin[3], u[3], v[3];
   double horizontal[3], vertical[3], lower_left[3];  // precomputed exactly as camera/mod.rs:99-108
+  // the image size as doubles and their correctly rounded reciprocals (host IEEE divisions): the
+  // jittered pixel's x / width as one correction step on x * (1 / width) (pixel_coord_div)
+  double wd, hd, inv_w, inv_h;
 };
 
 // Work decomposition: unit = (local tile, sample chunk, lane) ; see trace.hip.

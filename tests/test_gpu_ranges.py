@@ -192,24 +192,32 @@ def test_cli_progressive_checkpoints_and_resume(tmp_path):
 @pytest.mark.parametrize("change,why", [(["--seed", "0x5EEE"], "seed"), (["-m", "10"], "max_depth"),
                                         (["--sample-chunk", "4"], "sample_chunk"), (["-w", "40"], "x"),
                                         (["--camera-fov", "30"], "camera"), (["-s", "3"], "covers"),
-                                        (["--night"], "scene")])
+                                        (["@scene", "earth"], "scene")])
 def test_cli_resume_refuses_another_frame(tmp_path, change, why):
     """--resume continues only a checkpoint of the same frame — scene digest, camera, size,
     seed, max_depth and unit length equal, and no more samples done than the run renders; anything else
-    exits non-zero with the reason instead of adding the sums of another frame."""
+    exits non-zero with the reason instead of adding the sums of another frame.  (The demo scene does not
+    depend on the seed, so a changed seed is refused as a seed, not as another scene.)"""
     import os
     import subprocess
     from raytracer import _native as N
     cli = os.path.join(N.BIN_DIR, "ray-cli")
     ck = str(tmp_path / "ck.bin")
-    base = ["render", "random", "-w", "48", "-s", "4", "--seed", "0x5EED", "--sample-chunk", "2"]
+    base = ["render", "demo", "-w", "48", "-s", "4", "--seed", "0x5EED", "--sample-chunk", "2"]
     r = subprocess.run([cli] + base + ["-o", str(tmp_path / "a.png"), "--dump-accum", ck], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     argv = base[:] + ["-o", str(tmp_path / "b.png"), "--resume", ck, "--progressive", "1"]
-    for i in range(0, len(change), 2):
-        if change[i] in argv:
-            argv[argv.index(change[i]) + 1] = change[i + 1]
-        else:
-            argv += change[i:i + 2]
+    if change[0] == "@scene":
+        argv[1] = change[1]
+    elif change[0] in argv:
+        argv[argv.index(change[0]) + 1] = change[1]
+    else:
+        argv += change
     r = subprocess.run([cli] + argv, capture_output=True, text=True)
     assert r.returncode != 0 and why in r.stderr, r.stderr
+    # and the same checkpoint resumes as the same frame
+    ok = base[:]
+    ok[ok.index("-s") + 1] = "6"
+    r = subprocess.run([cli] + ok + ["-o", str(tmp_path / "c.png"), "--resume", ck, "--progressive", "1"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr

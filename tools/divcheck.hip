@@ -38,6 +38,14 @@ __global__ void check(uint64_t base, unsigned long long* bad) {
   // box faces divide through it, rt_device.h rect_t<.., INV>)
   const double g = div_recip(a, Recip{b, 1.0 / b});
   if (__double_as_longlong(q) != __double_as_longlong(g)) atomicAdd(&bad[3], 1ull);
+  // the traversal's 1 / d (rt_device.h inv_dir): the compiler's 1.0 / b against div_recip(1, recip(b))
+  // for |b| in [2^-300, 2^300] (inv_dir's fast path), special values included through inv_dir itself
+  const unsigned sp = (unsigned)(h3 >> 58) & 15u;  // special components now and then (inv_dir's fallback)
+  const double bs = sp == 0 ? 0.0 : sp == 1 ? -0.0 : sp == 2 ? __builtin_inf() : sp == 3 ? 1e-310 : sp == 4 ? 0x1p-301 : b;
+  const v3 iv = inv_dir(V(bs, a, b));
+  if (__double_as_longlong(1.0 / bs) != __double_as_longlong(iv.x) || __double_as_longlong(1.0 / a) != __double_as_longlong(iv.y) ||
+      __double_as_longlong(1.0 / b) != __double_as_longlong(iv.z))
+    atomicAdd(&bad[4], 1ull);
   // unit vectors: component exponents within +-40 of a common one
   const int ec = (int)((h3 >> 32) % 521) - 260;
   const uint64_t g1 = mix(i * 5 + 11), g2 = mix(i * 5 + 12), g3 = mix(i * 5 + 13);
@@ -69,15 +77,15 @@ int main(int argc, char** argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 26;
   const int launches = argc > 2 ? atoi(argv[2]) : 16;
   unsigned long long* bad;
-  if (hipMalloc(&bad, 32) != hipSuccess) return 2;
-  (void)hipMemset(bad, 0, 32);
+  if (hipMalloc(&bad, 40) != hipSuccess) return 2;
+  (void)hipMemset(bad, 0, 40);
   const uint64_t per = 1ull << lg;
   for (int l = 0; l < launches; ++l)
     hipLaunchKernelGGL(check, dim3((unsigned)(per / 256)), dim3(256), 0, 0, (uint64_t)l * per, bad);
-  unsigned long long h[4];
-  if (hipMemcpy(h, bad, 32, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+  unsigned long long h[5];
+  if (hipMemcpy(h, bad, 40, hipMemcpyDeviceToHost) != hipSuccess) return 2;
   printf("divcheck: %llu pairs, %llu division mismatches, %llu unit mismatches, %llu sqrt mismatches, "
-         "%llu inverse-division mismatches\n",
-         (unsigned long long)(per * launches), h[0], h[1], h[2], h[3]);
-  return (h[0] || h[1] || h[2] || h[3]) ? 1 : 0;
+         "%llu inverse-division mismatches, %llu reciprocal mismatches\n",
+         (unsigned long long)(per * launches), h[0], h[1], h[2], h[3], h[4]);
+  return (h[0] || h[1] || h[2] || h[3] || h[4]) ? 1 : 0;
 }

@@ -53,7 +53,7 @@ def main():
                 buf = torch.zeros((max_tiles, 64, 3), dtype=torch.float64, device="cuda")
             else:
                 buf = torch.zeros((cam.image_height, cam.image_width, 3), dtype=torch.float64, device="cuda")
-            ms, segs, chunks, passes = [], [], [], []
+            ms, segs, chunks, passes, kms, rms = [], [], [], [], [], []
             for r in range(world):
                 if part == "tiles":
                     s = rt.RenderSettings(samples=a.spp, seed=seed, tile_rank=r, tile_world=world, sample_chunk=a.chunk)
@@ -69,8 +69,11 @@ def main():
                         dev.render_device(cam, s, buf.data_ptr())
                     c = dev.counters()
                     t = c.kernel_ms + c.reduce_ms
-                    best = t if best is None else min(best, t)
+                    if best is None or t < best:
+                        best, bk, br = t, c.kernel_ms, c.reduce_ms
                 ms.append(best)
+                kms.append(bk)
+                rms.append(br)
                 segs.append(int(c.segments))
                 chunks.append(int(c.sample_chunk))
                 passes.append(int(c.passes))
@@ -88,7 +91,8 @@ def main():
                 xch = 2 * per_link_mb / LINK_GBS + frame_mb / world / HBM_GBS
             mx, mean = max(ms), sum(ms) / len(ms)
             out[str(world)] = {
-                "rank_device_ms": [round(x, 3) for x in ms], "rank_segments": segs,
+                "rank_device_ms": [round(x, 3) for x in ms], "rank_trace_ms": [round(x, 3) for x in kms],
+                "rank_reduce_ms": [round(x, 3) for x in rms], "rank_segments": segs,
                 "sample_chunk": sorted(set(chunks)), "passes": sorted(set(passes)),
                 "max_over_mean": round(mx / mean, 4),
                 "segments_max_over_mean": round(max(segs) / (sum(segs) / len(segs)), 4),
