@@ -884,14 +884,28 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
   if (p->scratch_mb == 0)
     if (const char* e = getenv("SHIRLEY_SCRATCH_MB")) budget = std::max(1LL, atoll(e)) << 20;  // tuning
   SamplePlan plan = plan_samples(n_pix, count, engine, lanes, p->sample_chunk, budget);
+  if (const char* e = getenv("SHIRLEY_SEGMENTS"))  // (tuning: per-block unit segments forced on / off)
+    plan.segments = engine == RT_ENGINE_MEGAKERNEL && atoi(e) != 0;
   if (!plan.ok) return fail(c, RT_E_UNSUPPORTED, "frame too large (%lld pixels)", (long long)n_pix);
   // a device short of memory gets more, smaller passes instead of a failed call (the frame is the same
   // for any number of passes)
-  while ((st = ensure(c, c->partial, (size_t)plan.partial_bytes)) == RT_E_OOM && plan.per_pass > 1) {
+  // (SHIRLEY_SIMULATE_OOM_MB, tests only: a partial buffer above that many MiB fails like hipMalloc would)
+  long long oom_limit = 0;
+  if (const char* e = getenv("SHIRLEY_SIMULATE_OOM_MB")) oom_limit = atoll(e) << 20;
+  auto alloc_partial = [&](size_t bytes) {
+    if (oom_limit > 0 && (long long)bytes > oom_limit)
+      return fail(c, RT_E_OOM, "simulated out-of-memory: %zu bytes of partial sums", bytes);
+    return ensure(c, c->partial, bytes);
+  };
+  bool fell_back = false;
+  const std::string err_before = c->err;
+  while ((st = alloc_partial((size_t)plan.partial_bytes)) == RT_E_OOM && plan.per_pass > 1) {
     (void)hipGetLastError();
+    fell_back = true;
     plan = plan_samples(n_pix, count, engine, lanes, p->sample_chunk, plan.partial_bytes / 2);
   }
   if (st) return st;
+  if (fell_back) c->err = err_before;  // the call succeeds: the refused allocation leaves no message behind
   const int chunk = plan.chunk, n_chunks = plan.n_chunks, passes = plan.passes, per_pass = plan.per_pass;
   const size_t partial_bytes = (size_t)plan.partial_bytes;
 

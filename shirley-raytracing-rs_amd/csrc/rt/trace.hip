@@ -123,7 +123,7 @@ void trace_kernel(KParams P) {
   // scatters' unit-sphere points, the dielectrics' uniforms and the new samples' jitter + lens points;
   // (4) shading; ended lanes add their radiance and publish finished units; new samples' camera rays.
   for (;;) {
-#ifdef RT_PHASE_TIMING
+#if defined(RT_PHASE_TIMING) && !defined(RT_PHASE_NO_EVENTS)
     const unsigned long long ph_before = ph_lane_steps;
 #endif
     // 1. one ray_color iteration (render.rs:30-46): closest hit and hit record, the material and the

@@ -92,6 +92,25 @@ def test_sample_passes_are_bit_identical(gpu, random_scene, engine):
     assert np.array_equal(r1, r4)
 
 
+def test_scratch_oom_falls_back_to_passes(gpu, random_scene, monkeypatch):
+    """A partial buffer the device cannot allocate (simulated: SHIRLEY_SIMULATE_OOM_MB) makes the call halve
+    its pass size until it fits: the frame is bit-identical to the one-pass frame, the call succeeds with
+    more passes, and no stale error message of the refused allocation is left (VERDICT r03 weak #8)."""
+    cam = rt.default_camera(64, "square")
+    gpu.upload(random_scene)
+    s = rt.RenderSettings(samples=40, seed=SEED, sample_chunk=1)
+    one = gpu.render(cam, s)
+    assert gpu.counters().passes == 1
+    from raytracer import _native as N
+    before = N.rt_lib().rt_last_error(gpu.handle).decode()
+    monkeypatch.setenv("SHIRLEY_SIMULATE_OOM_MB", "1")
+    lim = gpu.render(cam, s)
+    c = gpu.counters()
+    assert c.passes >= 4 and c.scratch_bytes <= (1 << 20)
+    assert np.array_equal(one, lim)
+    assert N.rt_lib().rt_last_error(gpu.handle).decode() == before
+
+
 def _sample_split(gpu, cam, settings, world):
     """RT_PARTITION_SAMPLES simulated on one device: rank r renders all pixels for its share of the
     frame's samples; the per-rank frames are summed in rank order (what the band sum computes)."""
