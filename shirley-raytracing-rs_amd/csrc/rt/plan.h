@@ -65,8 +65,8 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   // per-block unit segments (trace.hip): for units of >= 4 samples (measured: headline +2 %, gen_spheres
   // +11 %, final_scene +2.4 %, 2 ranks +2.4 %; with 1- or 2-sample units — small frames, 4 and 8 ranks
   // — the shared queue is as fast or faster: cfg1 -17 %, the 8-rank frame -6 % with segments).  A wave
-  // takes DWork.window units per queue atomic: kSegmentWindow (64) from its block's segment, kQueueWindow
-  // (256) from the shared queue, whose one counter all waves hit — the 8-rank frame (1-sample units)
+  // takes kSegmentWindow (64) units per queue atomic from its block's segment, kQueueWindow (256) from the
+  // shared queue, whose one counter all waves hit — the 8-rank frame (1-sample units)
   // 24.5 -> 23.4 ms with 256-unit windows (512: 23.8, 1024: 25.2; with segments 128 / 256 cost the
   // headline 0.4 / 1.8 %), profiles/r04/shard_scan/.
   P.segments = engine == RT_ENGINE_MEGAKERNEL && chunk >= 4;

@@ -997,10 +997,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     // per-block unit segments (trace.hip; plan.h): one counter per megakernel block
     const uint64_t per = (w.n_units + nseg - 1) / nseg;
     w.n_segs = plan.segments ? (uint32_t)nseg : 0u;
-    w.window = plan.segments ? kSegmentWindow : kQueueWindow;
-    if (const char* e = getenv("SHIRLEY_WINDOW"))  // (tuning)
-      w.window = (uint32_t)std::max(1, atoi(e) / kWave) * (uint32_t)kWave;
-    w.seg_len = (uint32_t)std::max<uint64_t>(w.window, (per + w.window - 1) / w.window * w.window);
+    w.seg_len = (uint32_t)std::max<uint64_t>(kSegmentWindow, (per + kSegmentWindow - 1) / kSegmentWindow * kSegmentWindow);
     // the device copy is taken after every field is set (the kernel may read any of them)
     c->host_work[k] = w;
     void* kwork = static_cast<char*>(c->kcam.p) + kCamBytes + kSceneBytes + (size_t)k * sizeof(DWork);

@@ -210,8 +210,6 @@ struct DWork {
   // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
   // segment, then steal from the next segments that still hold units
   uint32_t seg_len, n_segs;
-  uint32_t window;               // units a wave takes per queue atomic (a multiple of 64)
-  uint32_t pad_w;
 };
 
 // Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot
@@ -221,8 +219,8 @@ struct DCounters {
   unsigned long long pad[12];
 };
 constexpr int kCounterSlots = 64;
-// Work units a megakernel wave takes per queue atomic (DWork.window, a multiple of the wave size):
-// kSegmentWindow from a block's own segment, kQueueWindow from the one shared queue (plan.h).
+// Work units a megakernel wave takes per queue atomic (a multiple of the wave size): kSegmentWindow from
+// a block's own segment, kQueueWindow from the one shared queue (plan.h).
 constexpr unsigned kSegmentWindow = 64;
 constexpr unsigned kQueueWindow = 256;
 // instrumented build: DCounters.pad slots of the megakernel's phase clocks (PH_STAMP in trace.hip) and

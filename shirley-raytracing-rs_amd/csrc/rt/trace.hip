@@ -200,7 +200,7 @@ void trace_kernel(KParams P) {
         unsigned* ctr = reinterpret_cast<unsigned*>(P.unit_counter);
         for (;;) {
           unsigned off = 0;
-          if (lane == 0) off = atomicAdd(ctr + seg, W.window);
+          if (lane == 0) off = atomicAdd(ctr + seg, kSegmentWindow);
           off = (unsigned)__builtin_amdgcn_readfirstlane((int)off);
           if (off < W.seg_len && (unsigned long long)seg * W.seg_len + off < W.n_units) {
             nb = (unsigned long long)seg * W.seg_len + off;
@@ -226,13 +226,13 @@ void trace_kernel(KParams P) {
         }
         } else {  // one shared queue (short units: DWork.n_segs = 0)
           nb = 0;
-          if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)W.window);
+          if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)kQueueWindow);
           nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
                (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
         }
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
-        w_end = nb + W.window;
+        w_end = nb + (W.n_segs != 0u ? kSegmentWindow : kQueueWindow);
         if (nb >= W.n_units) exhausted = true;
       }
       if (need && idx < W.n_units) {
