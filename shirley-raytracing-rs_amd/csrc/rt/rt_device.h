@@ -1050,7 +1050,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
 // and skipped on pop when beyond the closest hit.
 // A child is one 32-bit word: its f32 entry t (> 0, so its bits order like the value) with the low K
 // bits (S.key_mask) replaced by the node index — a lower bound of the entry, so culling with it stays
-// conservative; misses, leaves and empty slots are ~0u.  Sorting is then 5 min/max pairs, a stack
+// conservative; misses, leaves and empty slots are ~0u.  Ordering is then 4 min/max pairs, a stack
 // entry is one word, and the cull `entry <= tmaxf` is one unsigned compare against bits(tmaxf) | mask.
 // tmaxf >= t_best: the cull may keep a subtree the exact comparison would drop, never the reverse, and
 // extra visits cannot change the closest hit (leaf tests are exact).  `sp` is the stack offset in
@@ -1098,11 +1098,13 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   unsigned p1 = (__float_as_uint(k1) & ~km) | (unsigned)ch.y;
   unsigned p2 = (__float_as_uint(k2) & ~km) | (unsigned)ch.z;
   unsigned p3 = (__float_as_uint(k3) & ~km) | (unsigned)ch.w;
+  // four of the five exchanges of the sorting network: p0 the nearest, p3 the farthest, the middle pair
+  // left in either order (the last exchange bought fewer visits than it cost: +0.4 % without it,
+  // DESIGN.md §5; no ordering at all: -6.3 %)
   cas_u(p0, p1);
   cas_u(p2, p3);
   cas_u(p0, p2);
   cas_u(p1, p3);
-  cas_u(p1, p2);
   const unsigned lim = __float_as_uint(tmaxf) | km;  // tmaxf finite: inf entries fail
   // the stack's top entry lives in `top` (~0u: empty); a push moves the old top to LDS (so stk[0]
   // holds the ~0u sentinel under any pushed entry), a pop takes `top` and prefetches the next one

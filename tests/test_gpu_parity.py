@@ -502,7 +502,7 @@ CONFIG_BANDS = [("cfg1", "random", 400, "std16x9", 50, None, 225),      # the wh
 # The exception, config 5: a pixel's channel is bit-identical only if none of its 2000 paths meets an
 # ulp-level libm difference (the marble's sin, the media's log, the sphere u, v's acos / atan2 on the
 # earth and the cluster), so at 2000 samples per pixel ~2 % of channels carry one; the same 0.1 %
-# outlier-pixel bound still holds.  Measured fractions: profiles/r04/parity_fractions_configs.jsonl
+# outlier-pixel bound still holds.  Measured fractions: profiles/r04/parity_fractions.jsonl (cfg5: 0.981)
 # (DESIGN.md §2).
 CFG5_EXACT = 0.975
 
