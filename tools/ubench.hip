@@ -61,6 +61,18 @@ __global__ __launch_bounds__(1024) void kern(int n, unsigned long long* out, uns
       if (OP == 34) asm volatile("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(k) : "vcc");
       if (OP == 35) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(k), "s"(cm[i]));
       if (OP == 36) asm volatile("v_max_u32 %0, %0, %1" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]));
+      // lane-mask reads: VCC written by a compare right before / two selects on one compare / a stale VCC
+      // read through the VOP3 form / a compare into an SGPR pair then a VOP3 select
+      if (OP == 37) asm volatile("v_cmp_lt_u32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc\n v_cndmask_b32 %1, %1, %0, vcc" : "+v"(a[i]), "+v"(a[(i + 1) % CHAINS]) : : "vcc");
+      if (OP == 38) asm volatile("v_cndmask_b32_e64 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(a[(i + 1) % CHAINS]));
+      if (OP == 39) asm volatile("v_cmp_lt_u32_e64 %2, %0, %1\n s_nop 1\n v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[i]) : "v"(k), "s"(cm[i]));
+      if (OP == 40) asm volatile("s_mov_b64 vcc, %1\n v_cndmask_b32 %0, %0, %0, vcc" : "+v"(a[i]) : "s"(sm) : "vcc");
+      if (OP == 41) asm volatile("v_cmp_lt_u32 vcc, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(k) : "vcc");
+      if (OP == 42) asm volatile("v_cmp_lt_f32 vcc, %0, %1\n v_cndmask_b32 %0, %0, %1, vcc" : "+v"(a[i]) : "v"(k) : "vcc");
+      // the leaf tests' pattern: two compares combined by SALU, then two selects (VOP2 vs VOP3 form)
+      if (OP == 43) asm volatile("v_cmp_lt_u32 vcc, %0, %3\n v_cmp_gt_u32_e64 %2, %1, %3\n s_and_b64 vcc, vcc, %2\n v_cndmask_b32 %0, %0, %3, vcc\n v_cndmask_b32 %1, %1, %3, vcc" : "+v"(a[i]), "+v"(a[(i + 1) % CHAINS]), "=&s"(cm[i]) : "v"(k) : "vcc");
+      if (OP == 44) asm volatile("v_cmp_lt_u32 vcc, %0, %3\n v_cmp_gt_u32_e64 %2, %1, %3\n s_and_b64 vcc, vcc, %2\n v_cndmask_b32_e64 %0, %0, %3, vcc\n v_cndmask_b32_e64 %1, %1, %3, vcc" : "+v"(a[i]), "+v"(a[(i + 1) % CHAINS]), "=&s"(cm[i]) : "v"(k) : "vcc");
+      if (OP == 45) asm volatile("v_cmp_lt_u32 vcc, %0, %3\n v_cmp_gt_u32_e64 %2, %1, %3\n s_and_b64 %2, vcc, %2\n v_cndmask_b32_e64 %0, %0, %3, %2\n v_cndmask_b32_e64 %1, %1, %3, %2" : "+v"(a[i]), "+v"(a[(i + 1) % CHAINS]), "=&s"(cm[i]) : "v"(k) : "vcc");
     }
   }
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -102,9 +114,12 @@ int main(int argc, char** argv) {
                          "v_min_f64", "v_cmp_lt_f64", "ds_bpermute+wait", "v_mad_u32_u24", "v_mul_f64",
                          "v_cvt_f32_f64", "v_mov_b64", "v_bitop3_b32", "v_perm_b32", "v_add_u32", "v_mov_b32_dpp",
                          "2x v_cndmask_b32", "v_max3_f32", "v_lshl_add_u64", "cndmask_e64 s-mask", "cndmask vcc const",
-                         "cndmask_e64 s nb", "v_cmp_lt_u32 ->s", "cmp+cndmask vcc", "cndmask_e64 cm", "v_max_u32 nb"};
-  const int nops = 37;
-  double c[37];
+                         "cndmask_e64 s nb", "v_cmp_lt_u32 ->s", "cmp+cndmask vcc", "cndmask_e64 cm", "v_max_u32 nb",
+                         "cmp+2x cndmask vcc", "cndmask_e64 vcc", "cmp_e64+nop+cndmask", "s_mov vcc+cndmask",
+                         "cmp,2 add,cndmask", "cmp_f32+cndmask", "2cmp,s_and vcc,2 cnd32", "2cmp,s_and vcc,2 cnd64",
+                         "2cmp,s_and s,2 cnd64"};
+  const int nops = 46;
+  double c[46];
   c[0] = run<0>(n, blocks, d, sink); c[1] = run<1>(n, blocks, d, sink); c[2] = run<2>(n, blocks, d, sink);
   c[3] = run<3>(n, blocks, d, sink); c[4] = run<4>(n, blocks, d, sink); c[5] = run<5>(n, blocks, d, sink);
   c[6] = run<6>(n, blocks, d, sink); c[7] = run<7>(n, blocks, d, sink); c[8] = run<8>(n, blocks, d, sink);
@@ -117,7 +132,10 @@ int main(int argc, char** argv) {
   c[27] = run<27>(n, blocks, d, sink); c[28] = run<28>(n, blocks, d, sink); c[29] = run<29>(n, blocks, d, sink);
   c[30] = run<30>(n, blocks, d, sink); c[31] = run<31>(n, blocks, d, sink); c[32] = run<32>(n, blocks, d, sink);
   c[33] = run<33>(n, blocks, d, sink); c[34] = run<34>(n, blocks, d, sink); c[35] = run<35>(n, blocks, d, sink);
-  c[36] = run<36>(n, blocks, d, sink);
+  c[36] = run<36>(n, blocks, d, sink); c[37] = run<37>(n, blocks, d, sink); c[38] = run<38>(n, blocks, d, sink);
+  c[39] = run<39>(n, blocks, d, sink); c[40] = run<40>(n, blocks, d, sink); c[41] = run<41>(n, blocks, d, sink);
+  c[42] = run<42>(n, blocks, d, sink); c[43] = run<43>(n, blocks, d, sink); c[44] = run<44>(n, blocks, d, sink);
+  c[45] = run<45>(n, blocks, d, sink);
   printf("threads/block %d (%d waves per SIMD): SIMD cycles per wave-instruction\n", g_threads, g_threads / 256);
   for (int i = 0; i < nops; ++i) printf("%-18s %6.2f\n", names[i], c[i]);
   return 0;
