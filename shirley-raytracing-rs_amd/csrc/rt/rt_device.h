@@ -85,12 +85,16 @@ __device__ __forceinline__ v3 unit_fast(v3 a) {
 // every |d_i| in [2^-300, 2^300] the compiler's own division sequence reduces to div_recip(1, recip(d_i))
 // (see Recip; checked on the GPU by tools/divcheck.hip), 7 instructions instead of 11; one range test
 // for the three components, the division itself otherwise (0, inf, NaN, extreme magnitudes).
-__device__ __forceinline__ v3 inv_dir(v3 d) {
+__device__ __forceinline__ v3 inv_dir(v3 d, bool& in_range) {
   const double lo = fmin(fmin(fabs(d.x), fabs(d.y)), fabs(d.z));
   const double hi = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
-  if (lo >= 0x1p-300 && hi <= 0x1p300)
-    return V(div_recip(1.0, recip(d.x)), div_recip(1.0, recip(d.y)), div_recip(1.0, recip(d.z)));
+  in_range = lo >= 0x1p-300 && hi <= 0x1p300;
+  if (in_range) return V(div_recip(1.0, recip(d.x)), div_recip(1.0, recip(d.y)), div_recip(1.0, recip(d.z)));
   return V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+}
+__device__ __forceinline__ v3 inv_dir(v3 d) {
+  bool in_range;
+  return inv_dir(d, in_range);
 }
 __device__ __forceinline__ double comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
 // vec3.rs:129-132
@@ -313,11 +317,22 @@ __device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Re
   return true;
 }
 
+// (k - o) / d of a face plane, bit-identical to the IEEE quotient: with every |d_i| in [2^-300, 2^300] (`ok`,
+// traverse4) and inv = the ray's 1/d (each component the correctly rounded reciprocal, inv_dir), Markstein's
+// correction of num * (1/d) (div_recip with y = RN(1/d)) is the correctly rounded quotient for |num| <= 2^700
+// (no intermediate overflows or underflows for any quotient the caller can accept: t >= t_min > 0 keeps
+// |num| >= 2^-310; tools/divcheck.hip checks it on the GPU); other operands divide.  3 VALU instead of 11.
+// (+1.1 % headline, +3.6 % Cornell: the coat and the Cornell boxes are RectBoxes, six faces per trip)
+__device__ __forceinline__ double face_div(double num, double den, double inv, bool ok) {
+  if (ok && fabs(num) <= 0x1p700) return div_recip(num, Recip{den, inv});
+  return num / den;
+}
 // rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset
 template <int D1, int D2>
-__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out) {
+__device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out,
+                                       v3 inv = v3{0.0, 0.0, 0.0}, bool ok = false) {
   constexpr int n = 3 - D1 - D2;
-  double t = (q[4] - comp(o, n)) / comp(d, n);
+  double t = face_div(q[4] - comp(o, n), comp(d, n), comp(inv, n), ok);
   if (t < t_min || t > t_max) return false;
   double d1v = comp(o, D1) + t * comp(d, D1);
   double d2v = comp(o, D2) + t * comp(d, D2);
@@ -328,28 +343,29 @@ __device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min
 
 // rect.rs:132-156 RectBox::hit — six faces in order, each against the running closest.
 // Returns the face index (0..5) that won, or -1.
-__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out) {
+__device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, double t_max, double& t_out,
+                                     v3 inv = v3{0.0, 0.0, 0.0}, bool ok = false) {
   double q[5];
   int face = -1;
   double tc = t_max, t;
   // xy_sides: (p0.x, p1.x, p0.y, p1.y, p1.z), (..., p0.z)
   q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
   q[4] = b[5];
-  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 0; }
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 0; }
   q[4] = b[2];
-  if (rect_t<0, 1>(q, o, d, t_min, tc, t)) { tc = t; face = 1; }
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 1; }
   // yz_sides: (p0.y, p1.y, p0.z, p1.z, p1.x), (..., p0.x)
   q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
   q[4] = b[3];
-  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 2; }
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 2; }
   q[4] = b[0];
-  if (rect_t<1, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 3; }
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 3; }
   // xz_sides: (p0.x, p1.x, p0.z, p1.z, p1.y), (..., p0.y)
   q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
   q[4] = b[4];
-  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 4; }
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 4; }
   q[4] = b[1];
-  if (rect_t<0, 2>(q, o, d, t_min, tc, t)) { tc = t; face = 5; }
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 5; }
   t_out = tc;
   return face;
 }
@@ -981,6 +997,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
   const unsigned nf = ~top_bytes((unsigned)c0, (unsigned)c1, (unsigned)c2, (unsigned)c3);
   const unsigned gm = (nf << 2) & 0x80808080u, bm = (nf << 3) & 0x80808080u;
   unsigned sph = lm & ~gm, rect = lm & gm & ~bm, box = lm & bm;
+  const bool div_ok = ra_ok;  // every |d_i| in range too (traverse4): faces divide through inv (face_div)
   bool hit = false;
   // nodes in LDS: child k's word read back from the node (one address op and one ds_read) instead of
   // the select chain over c0..c3 (+0.3 %)
@@ -1016,9 +1033,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     RT_STAT(++ptests);
     bool h;
     switch (pr.kind) {
-      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t); break;
-      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t); break;
-      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t);
+      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
+      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
+      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok);
     }
     if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
@@ -1039,7 +1056,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     }
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
     RT_STAT(++ptests);
-    const int f = box_t(pr.p, o, d, t_min, t_best, t);
+    const int f = box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
   if (hit) tmaxf = tmax_f32(t_best);
@@ -1161,12 +1178,14 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
 #endif
                                          ) {
   PH_COUNT(23);
-  const v3 inv = inv_dir(d);
+  bool inv_ok;
+  const v3 inv = inv_dir(d, inv_ok);
   const RaySigns ns = ray_signs(inv);
   const RayF rf = ray_f<typename Node4Sel<EXT>::T>(S, o, inv);
   const double a = len2(d);
   const Recip ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_r)
-  const bool ra_ok = a >= 0x1p-300 && a <= 0x1p300;
+  // the shared-reciprocal divisions' operand ranges: a (sphere roots) and every |d_i| (face planes, face_div)
+  const bool ra_ok = inv_ok && a >= 0x1p-300 && a <= 0x1p300;
   float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;
@@ -1199,11 +1218,12 @@ struct Trav4 {
 
 template <bool EXT>
 __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 d, double t_max) {
-  T.inv = inv_dir(d);
+  bool inv_ok;
+  T.inv = inv_dir(d, inv_ok);
   T.ns = ray_signs(T.inv);
   T.rf = ray_f<typename Node4Sel<EXT>::T>(S, o, T.inv);
   T.ra = recip(len2(d));
-  T.ra_ok = T.ra.b >= 0x1p-300 && T.ra.b <= 0x1p300;
+  T.ra_ok = inv_ok && T.ra.b >= 0x1p-300 && T.ra.b <= 0x1p300;
   T.t_best = t_max;
   T.tmaxf = tmax_f32(t_max);
   T.best = -1;

@@ -17,4 +17,4 @@ def test_shared_reciprocal_division_is_bit_identical():
     r = subprocess.run([BIN, "24", "8"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert (" 0 division mismatches, 0 unit mismatches, 0 sqrt mismatches, 0 inverse-division mismatches, "
-            "0 reciprocal mismatches") in r.stdout, r.stdout
+            "0 reciprocal mismatches, 0 face-division mismatches") in r.stdout, r.stdout

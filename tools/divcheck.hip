@@ -38,6 +38,11 @@ __global__ void check(uint64_t base, unsigned long long* bad) {
   // box faces divide through it, rt_device.h rect_t<.., INV>)
   const double g = div_recip(a, Recip{b, 1.0 / b});
   if (__double_as_longlong(q) != __double_as_longlong(g)) atomicAdd(&bad[3], 1ull);
+  // face planes (rt_device.h face_div): numerators with exponents in [-310, 700] (every numerator of a
+  // quotient >= t_min = 0.001 with |d| >= 2^-300, up to face_div's 2^700 bound) over the same divisors
+  const int ef = (int)((h3 >> 40) % 1011) - 310;
+  const double af = make(h1, ef);
+  if (__double_as_longlong(af / b) != __double_as_longlong(face_div(af, b, 1.0 / b, true))) atomicAdd(&bad[5], 1ull);
   // the traversal's 1 / d (rt_device.h inv_dir): the compiler's 1.0 / b against div_recip(1, recip(b))
   // for |b| in [2^-300, 2^300] (inv_dir's fast path), special values included through inv_dir itself
   const unsigned sp = (unsigned)(h3 >> 58) & 15u;  // special components now and then (inv_dir's fallback)
@@ -77,15 +82,15 @@ int main(int argc, char** argv) {
   const int lg = argc > 1 ? atoi(argv[1]) : 26;
   const int launches = argc > 2 ? atoi(argv[2]) : 16;
   unsigned long long* bad;
-  if (hipMalloc(&bad, 40) != hipSuccess) return 2;
-  (void)hipMemset(bad, 0, 40);
+  if (hipMalloc(&bad, 48) != hipSuccess) return 2;
+  (void)hipMemset(bad, 0, 48);
   const uint64_t per = 1ull << lg;
   for (int l = 0; l < launches; ++l)
     hipLaunchKernelGGL(check, dim3((unsigned)(per / 256)), dim3(256), 0, 0, (uint64_t)l * per, bad);
-  unsigned long long h[5];
-  if (hipMemcpy(h, bad, 40, hipMemcpyDeviceToHost) != hipSuccess) return 2;
+  unsigned long long h[6];
+  if (hipMemcpy(h, bad, 48, hipMemcpyDeviceToHost) != hipSuccess) return 2;
   printf("divcheck: %llu pairs, %llu division mismatches, %llu unit mismatches, %llu sqrt mismatches, "
-         "%llu inverse-division mismatches, %llu reciprocal mismatches\n",
-         (unsigned long long)(per * launches), h[0], h[1], h[2], h[3], h[4]);
-  return (h[0] || h[1] || h[2] || h[3] || h[4]) ? 1 : 0;
+         "%llu inverse-division mismatches, %llu reciprocal mismatches, %llu face-division mismatches\n",
+         (unsigned long long)(per * launches), h[0], h[1], h[2], h[3], h[4], h[5]);
+  return (h[0] || h[1] || h[2] || h[3] || h[4] || h[5]) ? 1 : 0;
 }
