@@ -1125,6 +1125,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     // a sphere's 1 / radius (sphere.rs:48 `scale(1.0 / self.radius)`), the same IEEE quotient the device
     // would compute per hit record; p[4] is otherwise unused by spheres
     if (q.kind == kPrimSphere || q.kind == kPrimMovingSphere) q.p[4] = 1.0 / q.p[3];
+    if (q.kind == kPrimSphere) {
+      // the sure-pass bound of the sphere's box test (rt_device.h leaf_tests4): r - eta rounded down, eta =
+      // 2^-48 (B + L) (B the largest box plane, L the fast-ray origin bound), or 0 (never sure)
+      const double eta = std::ldexp(infl.box_bound + (double)infl.origin_limit, -48);
+      const double rs = q.p[3] - eta;
+      q.p[5] = (std::isfinite(rs) && rs > 0.0) ? std::nextafter(rs, 0.0) : 0.0;
+    }
     q.material = o.material;
     if (is_extended(o)) {
       if (exts.size() >= (1u << (31 - kPrimExtShift)))
@@ -1155,6 +1162,17 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     for (int k = 0; k < 3; ++k) q.albedo[k] = m.albedo[k];
     q.param = m.param;
     q.inv_param = 1.0 / m.param;  // IEEE division: the bits dielectric.rs:27 computes per hit
+    if (m.kind == RT_MAT_DIELECTRIC) {
+      // Schlick's r0^2 (dielectric.rs:15-19) for the two ratios a hit can have — front face 1 / ir, back face
+      // ir — with the reference's operations (host and device are both IEEE binary64 without contraction), so
+      // the megakernel's reflectance skips a division per hit; a dielectric has no albedo (its attenuation is 1)
+      const double ratios[2] = {q.inv_param, m.param};
+      for (int k = 0; k < 2; ++k) {
+        double r0 = (1.0 - ratios[k]) / (1.0 + ratios[k]);
+        q.albedo[k] = r0 * r0;
+      }
+      q.albedo[2] = 0.0;
+    }
   }
   std::vector<DTex> texs(std::max(1, d->n_textures));
   for (int i = 0; i < d->n_textures; ++i) {

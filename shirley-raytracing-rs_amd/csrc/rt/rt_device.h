@@ -293,15 +293,34 @@ __device__ __forceinline__ bool sphere_t(const double* p, v3 o, v3 d, double a, 
   t = root;
   return true;
 }
-// The same with both root divisions by a through a per-ray shared reciprocal (exact: div_recip's
-// range, checked per numerator; a itself is in range when ra_ok).
+
+// (k - o) / d of a face plane, bit-identical to the IEEE quotient: with every |d_i| in [2^-300, 2^300] (`ok`,
+// traverse4) and inv = the ray's 1/d (each component the correctly rounded reciprocal, inv_dir), Markstein's
+// correction of num * (1/d) (div_recip with y = RN(1/d)) is the correctly rounded quotient for |num| <= 2^700
+// (no intermediate overflows or underflows for any quotient the caller can accept: t >= t_min > 0 keeps
+// |num| >= 2^-310; tools/divcheck.hip checks it on the GPU); other operands divide.  3 VALU instead of 11.
+// (+1.1 % headline, +3.6 % Cornell: the coat and the Cornell boxes are RectBoxes, six faces per trip; DESIGN.md §5)
+__device__ __forceinline__ double face_div(double num, double den, double inv, bool ok) {
+  if (ok && fabs(num) <= 0x1p700) return div_recip(num, Recip{den, inv});
+  return num / den;
+}
+// Root division by a through the per-ray shared reciprocal (exact: div_recip's range, checked per numerator;
+// a itself is in range when ra_ok).
 __device__ __forceinline__ double div_by(double n, const Recip& R, bool ok) {
   const double m = fabs(n);
   if (ok && m >= 0x1p-300 && m <= 0x1p300) return div_recip(n, R);
   return n / R.b;
 }
-__device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Recip& ra, bool ra_ok, double t_min,
-                                           double t_max, double& t) {
+// sphere.rs:28-46 (t only), both root divisions through div_by, that also says whether the sphere's box test
+// (aabb.rs:62-79 hit2 on c -+ r) surely passes for the root it returns: t_min < t < t_max, and the hit point relative to the centre, oc + t d (one fma per axis),
+// inside the box by the scene's rounding margin on every axis — p[5] = r - eta rounded down (host, rt_api.cpp;
+// <= 0 for radii too small or negative: never sure), eta = 2^-48 (B + L) with B the largest box plane and L the
+// origin bound of the f32 node test, which ra_ok includes (with every |d_i| >= 2^-300).  Then every entry and
+// exit the slab test computes lies strictly before / after t: DESIGN.md §3.1 has the error bound (it needs
+// ~2^-50 (B + L)), tests/sphere_sure_check.c the adversarial CPU check (no false pass; ~55 k false passes
+// without the margin).
+__device__ __forceinline__ bool sphere_t_sure(const double* p, v3 o, v3 d, const Recip& ra, bool ra_ok, double t_min,
+                                              double t_max, double& t, bool& sure) {
   v3 oc = o - V(p[0], p[1], p[2]);
   double half_b = dot(oc, d);
   double c = len2(oc) - p[3] * p[3];
@@ -314,19 +333,13 @@ __device__ __forceinline__ bool sphere_t_r(const double* p, v3 o, v3 d, const Re
     if (root < t_min || t_max < root) return false;
   }
   t = root;
+  const double p5 = p[5];
+  // (bitwise: one straight-line mask, no branches)
+  sure = (int)ra_ok & (int)(root > t_min) & (int)(root < t_max) & (int)(fabs(fma(root, d.x, oc.x)) < p5) &
+         (int)(fabs(fma(root, d.y, oc.y)) < p5) & (int)(fabs(fma(root, d.z, oc.z)) < p5);
   return true;
 }
 
-// (k - o) / d of a face plane, bit-identical to the IEEE quotient: with every |d_i| in [2^-300, 2^300] (`ok`,
-// traverse4) and inv = the ray's 1/d (each component the correctly rounded reciprocal, inv_dir), Markstein's
-// correction of num * (1/d) (div_recip with y = RN(1/d)) is the correctly rounded quotient for |num| <= 2^700
-// (no intermediate overflows or underflows for any quotient the caller can accept: t >= t_min > 0 keeps
-// |num| >= 2^-310; tools/divcheck.hip checks it on the GPU); other operands divide.  3 VALU instead of 11.
-// (+1.1 % headline, +3.6 % Cornell: the coat and the Cornell boxes are RectBoxes, six faces per trip; DESIGN.md §5)
-__device__ __forceinline__ double face_div(double num, double den, double inv, bool ok) {
-  if (ok && fabs(num) <= 0x1p700) return div_recip(num, Recip{den, inv});
-  return num / den;
-}
 // rect.rs:54-65 (t only): axes (D1, D2), normal axis n = 3-D1-D2; q = d1_min d1_max d2_min d2_max offset
 template <int D1, int D2>
 __device__ __forceinline__ bool rect_t(const double* q, v3 o, v3 d, double t_min, double t_max, double& t_out,
@@ -1016,8 +1029,16 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double t;
     PH_COUNT(3);
     RT_STAT(++ptests);
-    if (!sphere_t_r(pr.p, o, d, ra, ra_ok, t_min, t_best, t)) continue;
-    if (!slab_sphere(pr.p, o, inv, ns, t_min, t_best)) continue;
+    // The reference's `box.hit2 && sphere.hit`: the box test runs only where the sphere test hit and the
+    // rounding margin does not already prove that it passes (sphere_t_sure; +0.3 %).  The
+    // primitive is re-read for it, so no copy of c, r is held across the sphere test.
+    bool sure;
+    if (!sphere_t_sure(pr.p, o, d, ra, ra_ok, t_min, t_best, t, sure)) continue;
+    if (!sure) {
+      const DPrim* pp = &pr;
+      asm volatile("" : "+v"(pp));
+      if (!slab_sphere(pp->p, o, inv, ns, t_min, t_best)) continue;
+    }
     t_best = t; best = leaf; face_best = -1; hit = true;
   }
 #pragma unroll 1
@@ -1183,9 +1204,9 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
   const RaySigns ns = ray_signs(inv);
   const RayF rf = ray_f<typename Node4Sel<EXT>::T>(S, o, inv);
   const double a = len2(d);
-  const Recip ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_r)
+  const Recip ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_sure)
   // the shared-reciprocal divisions' operand ranges: a (sphere roots) and every |d_i| (face planes, face_div)
-  const bool ra_ok = inv_ok && a >= 0x1p-300 && a <= 0x1p300;
+  const bool ra_ok = inv_ok && a >= 0x1p-300 && a <= 0x1p300 && rf.fast;
   float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;
@@ -1206,7 +1227,7 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
 // Step-wise form for wf_extend4, where a ray's traversal state lives across loop iterations.
 struct Trav4 {
   v3 inv;
-  Recip ra;  // ra.b = |d|^2 (sphere_t_r)
+  Recip ra;  // ra.b = |d|^2 (sphere_t_sure)
   bool ra_ok;
   double t_best;
   float tmaxf;
@@ -1223,7 +1244,7 @@ __device__ __forceinline__ void trav4_begin(Trav4& T, const DScene& S, v3 o, v3 
   T.ns = ray_signs(T.inv);
   T.rf = ray_f<typename Node4Sel<EXT>::T>(S, o, T.inv);
   T.ra = recip(len2(d));
-  T.ra_ok = inv_ok && T.ra.b >= 0x1p-300 && T.ra.b <= 0x1p300;
+  T.ra_ok = inv_ok && T.ra.b >= 0x1p-300 && T.ra.b <= 0x1p300 && T.rf.fast;
   T.t_best = t_max;
   T.tmaxf = tmax_f32(t_max);
   T.best = -1;
@@ -1835,6 +1856,24 @@ __device__ __forceinline__ double reflectance_inl(double cosine, double ref_idx)
   return r0 + (1.0 - r0) * pow5(1.0 - cosine);
 }
 __device__ __noinline__ double reflectance(double cosine, double ref_idx) { return reflectance_inl(cosine, ref_idx); }
+// reflectance_inl with its r0^2 from the host (DMat: a dielectric's albedo[0] / albedo[1] for the front / back face)
+__device__ __noinline__ double pow5_libm(double x) { return pow(x, 5.0); }
+__device__ __forceinline__ double reflectance_r0sq(double cosine, double r0sq) {
+  const double x = 1.0 - cosine;
+  double p;
+  if (!(x >= 0.0 && x <= 4.0)) {
+    p = pow5_libm(x);
+  } else {
+    const double x2 = x * x;
+    const double x2l = fma(x, x, -x2);
+    const double x4 = x2 * x2;
+    const double x4l = fma(x2, x2, -x4) + (2.0 * x2) * x2l;
+    const double x5 = x4 * x;
+    const double x5l = fma(x4, x, -x5) + x4l * x;
+    p = x5 + x5l;
+  }
+  return r0sq + (1.0 - r0sq) * p;
+}
 
 // skybox/mod.rs:5-25
 // skybox/mod.rs:18-25 given un = unit(d)
@@ -1998,11 +2037,13 @@ __device__ __forceinline__ bool shade_factor(const DScene& S, const DMat& m, int
     double ratio = h.front_face ? m.inv_param : m.param;  // 1.0 / ir, precomputed
     const v3 ud = un;
     double cos_theta = fmin_one(dot(scale(ud, -1.0), h.normal));
-    double sin_theta = sqrt_rn(1.0 - cos_theta * cos_theta);
-    bool refl = ratio * sin_theta > 1.0;
+    // ratio * sin_theta > 1 (TIR) needs ratio > 1: sin_theta = sqrt(1 - cos^2) <= 1 (or NaN, which fails the
+    // compare) since cos^2 >= 0, so with ratio <= 1 — every front face, and both faces of an ir = 1 coat —
+    // the square root is skipped and the decision is the same
+    bool refl = ratio > 1.0 && ratio * sqrt_rn(1.0 - cos_theta * cos_theta) > 1.0;
     if (!refl) {  // drawn only if not TIR: the uniform drawn ahead by draws_coop is consumed
       PH_COUNT(22);
-      refl = reflectance(cos_theta, ratio) > r.x;
+      refl = reflectance_r0sq(cos_theta, h.front_face ? m.albedo[0] : m.albedo[1]) > r.x;
       const uint64_t cb = double_as_u64(r.y);
       rng.draw += 1u;
       rng.c2 = (uint32_t)cb;

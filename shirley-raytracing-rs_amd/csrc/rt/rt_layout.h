@@ -98,7 +98,7 @@ static_assert(sizeof(DExt) == 144, "DExt layout");
 
 // One primitive = one reference leaf object (a RectBox stays ONE leaf of 6 faces, rect.rs:146-156).
 struct alignas(16) DPrim {
-  double p[6];       // sphere: cx cy cz r 1/r ; rect: d1_min d1_max d2_min d2_max offset ; box: min xyz max xyz
+  double p[6];       // sphere: cx cy cz r 1/r sure-pass bound (r - eta) ; rect: d1_min d1_max d2_min d2_max offset ; box: min xyz max xyz
   int32_t kind;
   int32_t material;  // material index
 };
@@ -107,7 +107,7 @@ static_assert(sizeof(DPrim) == 64, "DPrim layout");
 struct alignas(16) DMat {
   int32_t kind;   // RT_MAT_*
   int32_t tex;
-  double albedo[3];
+  double albedo[3];  // Metal albedo; a Dielectric's Schlick r0^2 for its front / back face ratio (host-computed)
   double param;
   double inv_param;  // 1.0 / param, computed on the host (the dielectric's front-face ratio 1.0 / ir)
 };

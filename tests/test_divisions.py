@@ -15,3 +15,21 @@ def test_camera_coordinate_division_is_exact(tmp_path):
     r = subprocess.run([exe, "20000000"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout
     assert r.stdout.strip().startswith("0 of ")
+
+
+def test_sphere_sure_pass_never_skips_a_rejecting_box_test(tmp_path):
+    """The megakernel skips a sphere leaf's exact box test (aabb.rs:62-79 on c -+ r) where the rounding
+    margin proves it passes (rt_device.h leaf_tests4).  tests/sphere_sure_check.c draws
+    adversarial spheres and rays (hits at the box-face tangent points, rays tangent in the face planes,
+    origins on the sphere, axis-parallel directions): among ~190 k sphere hits whose box test rejects, the
+    rule must clear none — and it must still clear most hits, or the skip buys nothing.  (With no margin the
+    same draws give ~55 k false skips: the check has teeth.)"""
+    exe = str(tmp_path / "sphere_sure_check")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe, os.path.join(REPO, "tests", "sphere_sure_check.c"),
+                    "-lm"], check=True)
+    r = subprocess.run([exe, "8000000"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout
+    f = {k: int(v) for v, k in [(w.split()[0], " ".join(w.split()[1:])) for w in r.stdout.split(":")[1].split(",")]}
+    assert f["sure but box rejects"] == 0, r.stdout
+    assert f["box rejects among them"] > 100000, r.stdout
+    assert f["sure"] > 0.8 * f["sphere hits"], r.stdout
