@@ -1125,7 +1125,7 @@ __device__ __forceinline__ unsigned node4_visit(const DScene& S, const N4* lds_n
 }
 // visit4's ordering part: internal children as packed words (a miss, k = inf or ~0u, packs above any
 // bound), nearest first; the three farther ones pushed, the nearest returned, else the stack popped.
-template <int STRIDE>
+template <int STRIDE, bool FULL>
 __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, float k1, float k2, float k3,
                                           float tmaxf, int& sp, unsigned& top, unsigned* stk) {
   // No select needed for leaves and empty slots: a leaf's child word is negative (top bit set) and
@@ -1136,13 +1136,14 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   unsigned p1 = (__float_as_uint(k1) & ~km) | (unsigned)ch.y;
   unsigned p2 = (__float_as_uint(k2) & ~km) | (unsigned)ch.z;
   unsigned p3 = (__float_as_uint(k3) & ~km) | (unsigned)ch.w;
-  // four of the five exchanges of the sorting network: p0 the nearest, p3 the farthest, the middle pair
-  // left in either order (the last exchange bought fewer visits than it cost: +0.4 % without it,
-  // DESIGN.md §5; no ordering at all: -6.3 %)
+  // the sorting network; with the scene in LDS only four of its five exchanges: p0 the nearest, p3 the
+  // farthest, the middle pair left in either order (there the last exchange bought fewer visits than it
+  // cost: +0.4 % headline without it; scenes read through L2 lose 2-4 % without it)
   cas_u(p0, p1);
   cas_u(p2, p3);
   cas_u(p0, p2);
   cas_u(p1, p3);
+  if (FULL) cas_u(p1, p2);
   const unsigned lim = __float_as_uint(tmaxf) | km;  // tmaxf finite: inf entries fail
   // the stack's top entry lives in `top` (~0u: empty); a push moves the old top to LDS (so stk[0]
   // holds the ~0u sentinel under any pushed entry), a pop takes `top` and prefetches the next one
@@ -1184,7 +1185,7 @@ __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<E
   if (lm)
     leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
                            face_best, rk, seed, ptests);
-  return node4_next<STRIDE>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
+  return node4_next<STRIDE, MODE != kSceneLds>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
 }
 
 // Whole closest-hit query over the 4-wide tree (t_min > 0).  The conservative internal tests and the
