@@ -1041,25 +1041,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     }
     t_best = t; best = leaf; face_best = -1; hit = true;
   }
-#pragma unroll 1
-  while (rect) {
-    PH_COUNT(4);
-    const int k = __builtin_ctz(rect) >> 3;
-    rect &= rect - 1;
-    const int leaf = (~child(k)) & kLeafPrimMask;
-    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
-    double b[6], te, t;
-    leaf_box(pr, b);
-    if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
-    RT_STAT(++ptests);
-    bool h;
-    switch (pr.kind) {
-      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
-      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
-      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok);
-    }
-    if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
-  }
+  // RectBox leaves before rect leaves: a box in front of a rect (the random scene's ground coat over its
+  // lower surface, Cornell's blocks before its walls) then shrinks t_best first, so the rect's own box
+  // test rejects without the rect test (+0.25 % headline)
 #pragma unroll 1
   while (box) {
     PH_COUNT(7);
@@ -1079,6 +1063,25 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     RT_STAT(++ptests);
     const int f = box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
+  }
+#pragma unroll 1
+  while (rect) {
+    PH_COUNT(4);
+    const int k = __builtin_ctz(rect) >> 3;
+    rect &= rect - 1;
+    const int leaf = (~child(k)) & kLeafPrimMask;
+    const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
+    double b[6], te, t;
+    leaf_box(pr, b);
+    if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
+    RT_STAT(++ptests);
+    bool h;
+    switch (pr.kind) {
+      case kPrimRectXY: h = rect_t<0, 1>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
+      case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
+      default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok);
+    }
+    if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
   if (hit) tmaxf = tmax_f32(t_best);
 }
