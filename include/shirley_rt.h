@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 typedef enum rt_status {
   RT_OK = 0,
@@ -314,6 +314,27 @@ enum { RT_TRAVERSAL_BINARY = 0, RT_TRAVERSAL_RENDER = 1 };
 int rt_scene_hit_ex(rt_ctx* ctx, const double* rays, int32_t n, double t_min, double t_max, int32_t traversal,
                     rt_hit* out);
 
+/* ABI 7: one iteration of ray_color's loop (render.rs:30-46) for each given ray, through the megakernel's
+ * own device code — the render traversal (t in [0.001, inf)), the hit record, the material and its texture
+ * (Perlin marble evaluated by the wave), the wave's sampler for the scatter's draws, and the shading —
+ * with ray i on the path key (seed, pixel = i, sample, draw): emitted() and scatter() of the hit's material
+ * (material_type.rs:51-79), or the sky on a miss (skybox/mod.rs:5-25), and the path's draw counter after
+ * the segment.  A verification probe of the scatter semantics (tests/test_scatter_kat.py); book-2 ray time 0. */
+typedef struct rt_probe {
+  int32_t object;          /* closest object, -1: missed (the sky) */
+  int32_t front_face;
+  int32_t scattered;       /* scatter() returned Some: the path goes on along (origin, direction) */
+  int32_t emits;           /* emitted() returned Some (or the sky): `emitted` holds it */
+  uint32_t draw;           /* the path's draw counter after the segment */
+  int32_t pad;
+  double t, point[3], normal[3];
+  double emitted[3];
+  double attenuation[3];   /* scatter().attenuation */
+  double origin[3], direction[3];  /* scatter().direction: the next ray */
+} rt_probe;
+int rt_probe_segment(rt_ctx* ctx, const double* rays, int32_t n, uint64_t seed, uint32_t sample, uint32_t draw,
+                     rt_probe* out);
+
 /* ---- multi-GPU (ABI 4) -------------------------------------------------------
  * The frame's 8x8 tiles are dealt round-robin over the ranks of a communicator (tile k -> rank
  * k % world); each rank renders its tiles into a packed buffer and RCCL gathers the packed buffers to
@@ -321,14 +342,17 @@ int rt_scene_hit_ex(rt_ctx* ctx, const double* rays, int32_t n, double t_min, do
  * every rank renders all pixels for a share of the samples (RT_PARTITION_SAMPLES, see above).  The
  * counter RNG is keyed by the global pixel and sample, so a tile-sharded frame is bit-identical for every
  * world size given an explicit sample_chunk (the automatic chunk follows the rank's pixel count).  Every
- * ctx must hold the same scene and every rank must pass the same call arguments: rt_render_sharded
- * all-gathers each rank's (scene digest, call key) — the key hashes the resolved partition and sample
- * range, samples, seed, max_depth, sample_chunk and the camera — and fails with RT_E_INVALID on every rank
- * alike on a mismatch, before any collective of the frame.  The agreed key is cached on the communicator:
- * a call whose key equals it does no exchange and no host synchronisation (a loop of frames stays
- * asynchronous); ranks changing scene or arguments together re-check on that call.  (A rank that changes
- * them alone re-checks while the others proceed to the frame's collectives: that misuse stalls instead
- * of failing.)  rt_render_multi compares the digests on the host.  Replaces the
+ * ctx must hold the same scene and every rank must pass the same call arguments: every call of
+ * rt_render_sharded all-gathers each rank's (scene digest, call key) — the key hashes the resolved partition
+ * and sample range, samples, seed, max_depth, sample_chunk and the camera — so all ranks issue the same
+ * collective sequence whatever their arguments, and checks the gathered words on the host: in the call,
+ * before any collective of the frame, when this rank's key differs from the one the ranks last agreed on
+ * (ranks changing scene or arguments together all fail there with RT_E_INVALID on a mismatch); otherwise
+ * at the rank's next call, so a loop of frames needs no host round trip.  Misuse — one rank changing its
+ * key alone — fails that rank in the call; its peers have already issued the frame's collectives, which it
+ * never joins, so their stream waits (undefined from RCCL's side: do not rely on it).  SHIRLEY_KEY_CHECK=sync
+ * checks every call before the frame's collectives (every rank fails in the call itself, one host round
+ * trip per call).  rt_render_multi compares the digests on the host.  Replaces the
  * reference's whole-machine rayon loop over scanlines (main.rs:92-126).  RCCL is loaded on first use
  * (dlopen "librccl.so.1": the copy already in the process if any); without it these calls return
  * RT_E_RCCL.

@@ -1193,6 +1193,57 @@ void or_sample_color(const or_scene* s, const rt_camera* cam, const rt_render_pa
   free(w.stack);
 }
 
+/* one iteration of ray_color's loop (render.rs:30-46) for a given ray and path key: the closest hit
+ * (t in [0.001, inf)), material_type.rs:51-79's emitted and scatter, or the sky on a miss */
+void or_probe_segment(const or_scene* s, const double ray[6], uint64_t seed, uint32_t pixel, uint32_t sample,
+                      uint32_t draw, or_probe* out) {
+  ray_t r = ray_from(ray);
+  work_t w;
+  work_init(s, &w);
+  rng_t rng;
+  rng.seed = seed;
+  rng.pixel = pixel;
+  rng.sample = sample;
+  rng.draw = draw;
+  w.ctx.seed = seed;
+  w.ctx.pixel = pixel;
+  w.ctx.sample = sample;
+  w.ctx.draw = draw;
+  w.ctx.time0 = w.ctx.time1 = 0.0;
+  memset(out, 0, sizeof(*out));
+  out->object = -1;
+  hit_t h;
+  int32_t obj = -1;
+  if (scene_hit(s, &w, &r, 0.001, INFINITY, &h, &obj)) {
+    const rt_material* m = &s->materials[s->objects[obj].material];
+    out->object = obj;
+    out->front_face = h.front_face;
+    out->t = h.t;
+    out->point[0] = h.point.x; out->point[1] = h.point.y; out->point[2] = h.point.z;
+    out->normal[0] = h.normal.x; out->normal[1] = h.normal.y; out->normal[2] = h.normal.z;
+    v3 e;
+    if (material_emitted(s, m, &r, &h, &e)) {
+      out->emits = 1;
+      out->emitted[0] = e.x; out->emitted[1] = e.y; out->emitted[2] = e.z;
+    }
+    ray_t sc;
+    v3 att;
+    if (material_scatter(s, m, &rng, &r, &h, &sc, &att)) {
+      out->scattered = 1;
+      out->attenuation[0] = att.x; out->attenuation[1] = att.y; out->attenuation[2] = att.z;
+      out->origin[0] = sc.o.x; out->origin[1] = sc.o.y; out->origin[2] = sc.o.z;
+      out->direction[0] = sc.d.x; out->direction[1] = sc.d.y; out->direction[2] = sc.d.z;
+    }
+  } else {
+    v3 e = sky_background(s, &r);
+    out->emits = 1;
+    out->emitted[0] = e.x; out->emitted[1] = e.y; out->emitted[2] = e.z;
+  }
+  out->draw = rng.draw;
+  free(w.stack);
+}
+double or_reflectance(double cosine, double ref_idx) { return reflectance(cosine, ref_idx); }
+
 /* image.rs:31-44 + color.rs:31-38: (x * 255.999) as u8 saturates, NaN -> 0 */
 static uint8_t to_u8(double x) {
   double y = x * 255.999;

@@ -93,6 +93,15 @@ void or_render_scanline(const or_scene* s, const rt_camera* cam, const rt_render
 int32_t or_render_rows(const or_scene* s, const rt_camera* cam, const rt_render_params* p, int32_t line_begin,
                        int32_t line_end, int32_t nthreads, double* out, or_counters* cnt);
 
+/* one iteration of render.rs:30-46 (ray_color's loop body) for `ray` with the path key (seed, pixel,
+ * sample, draw): closest hit, emitted, scatter (material_type.rs:51-79) — or the sky on a miss; the
+ * layout of rt_probe (include/shirley_rt.h, the device's rt_probe_segment).  Book-2 ray time 0. */
+typedef rt_probe or_probe;
+void or_probe_segment(const or_scene* s, const double ray[6], uint64_t seed, uint32_t pixel, uint32_t sample,
+                      uint32_t draw, or_probe* out);
+/* dielectric.rs:15-19 */
+double or_reflectance(double cosine, double ref_idx);
+
 /* image.rs:31-44 + color.rs:31-38 */
 void or_tonemap(const double* accum, int32_t width, int32_t height, int32_t samples, uint8_t* rgb8);
 

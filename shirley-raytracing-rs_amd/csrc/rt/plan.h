@@ -22,6 +22,12 @@ constexpr int kWfDefaultChunk = 8;          // wavefront engine's unit length (i
 // per pass) where memory matters more than those milliseconds — the frame is bit-identical either way.
 constexpr long long kDefaultScratchMiB = 8192;
 
+// Work units a megakernel wave takes per queue atomic (multiples of the wave size): kSegmentWindow from a
+// block's own segment, and from the one shared queue kQueueWindow while many units remain, then
+// kSegmentWindow for the pool's last units (SamplePlan.queue_tail).
+constexpr unsigned kSegmentWindow = 64;
+constexpr unsigned kQueueWindow = 256;
+
 struct SamplePlan {
   int chunk = 1;          // samples per unit
   int n_chunks = 0;       // chunks of the call's range
@@ -29,7 +35,11 @@ struct SamplePlan {
   int passes = 0;
   long long partial_bytes = 0;  // scratch of one pass
   bool segments = false;  // megakernel per-block unit segments (units of >= 4 samples)
-  bool ok = true;         // false: a pass cannot index one chunk of the frame in 32 bits
+  // shared queue (segments off): a wave takes queue_window units per atomic while more than queue_tail
+  // units remain after its last window, kSegmentWindow after that
+  unsigned queue_window = kQueueWindow;
+  unsigned long long queue_tail = 0;
+  bool ok = true;        // false: a pass cannot index one chunk of the frame in 32 bits
 };
 
 // n_pix: pixels of the call's tiles (tiles x 64), count: samples in the range, lanes: resident megakernel
@@ -70,6 +80,12 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   // 24.5 -> 23.4 ms with 256-unit windows (512: 23.8, 1024: 25.2; with segments 128 / 256 cost the
   // headline 0.4 / 1.8 %), profiles/r04/shard_scan/.
   P.segments = engine == RT_ENGINE_MEGAKERNEL && chunk >= 4;
+  // The shared queue's windows shrink for the pool's end (guided self-scheduling): a wave's last window
+  // decides when it finishes, and 256 units are 4 per lane — on a small frame (cfg1 400x225 @ 50: 17
+  // units per lane) a ragged end of up to 4 units per lane.  So a wave takes 256-unit windows while more
+  // than one round of them (256 units per resident wave) remains, and 64-unit windows after that.
+  P.queue_window = kQueueWindow;
+  P.queue_tail = (unsigned long long)std::max(1LL, lanes / 64) * kQueueWindow;
 
   // sample passes: at most `budget` bytes of [chunks][pixels][3] f64 partial sums per pass
   const long long chunk_bytes = std::max<long long>(1, n_pix * 3 * (long long)sizeof(double));

@@ -16,6 +16,7 @@
 
 #include "../../../include/shirley_rt.h"
 #include "bvh_build.h"
+#include "keycheck.h"
 #include "plan.h"
 #include "rccl_loader.h"
 #include "rt_layout.h"
@@ -45,6 +46,8 @@ hipError_t launch_hit(const DScene& S, const double* rays, int n, double t_min, 
                       hipStream_t stream);
 hipError_t launch_hit4(const DScene& S, bool wide, const double* rays, int n, double t_min, double t_max, void* out,
                        hipStream_t stream);
+hipError_t launch_probe(const DScene& S, bool wide, const double* rays, int n, uint64_t seed, uint32_t sample,
+                        uint32_t draw, void* out, hipStream_t stream);
 // wavefront.hip
 size_t wf_extend_lds(int n_lds_nodes, int stack_depth);
 int wf_extend_threads();
@@ -69,10 +72,14 @@ struct DevBuf {
 struct rt_comm {
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0, device = 0;
-  // the call key (scene digest + resolved partition, sample range and the render arguments) every rank
-  // last agreed on; rt_render_sharded exchanges keys only when this rank's key differs from it
-  bool verified = false;
-  uint64_t verified_key = 0;
+  // rt_render_sharded's cross-rank check (keycheck.h): the key the ranks last agreed on, and the gathered
+  // (digest, key) words of the last two calls in pinned host memory ([2 slots][world + 1][2]: the gathered
+  // words, then this rank's own), each slot's copy marked by an event
+  KeyState ks;
+  uint64_t* key_words = nullptr;
+  hipEvent_t key_ev[2] = {nullptr, nullptr};
+  int key_slot = 0;       // slot of the next call
+  int key_pending = 0;    // slot of the pending (deferred) check
 };
 
 struct rt_ctx {
@@ -998,6 +1005,12 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     const uint64_t per = (w.n_units + nseg - 1) / nseg;
     w.n_segs = plan.segments ? (uint32_t)nseg : 0u;
     w.seg_len = (uint32_t)std::max<uint64_t>(kSegmentWindow, (per + kSegmentWindow - 1) / kSegmentWindow * kSegmentWindow);
+    w.q_window = plan.queue_window;
+    w.q_tail = plan.queue_tail;
+    if (const char* e = getenv("SHIRLEY_WINDOW"))  // (tuning: the shared queue's big window, units)
+      w.q_window = (uint32_t)std::max(1, atoi(e) / kWave) * (uint32_t)kWave;
+    if (const char* e = getenv("SHIRLEY_QUEUE_TAIL"))  // (tuning: units left below which windows are 64)
+      w.q_tail = (uint64_t)std::max(0LL, atoll(e));
     // the device copy is taken after every field is set (the kernel may read any of them)
     c->host_work[k] = w;
     void* kwork = static_cast<char*>(c->kcam.p) + kCamBytes + kSceneBytes + (size_t)k * sizeof(DWork);
@@ -1484,6 +1497,31 @@ int rt_scene_hit_ex(rt_ctx* c, const double* rays, int32_t n, double t_min, doub
   return st;
 }
 
+int rt_probe_segment(rt_ctx* c, const double* rays, int32_t n, uint64_t seed, uint32_t sample, uint32_t draw,
+                     rt_probe* out) {
+  if (!c) return RT_E_INVALID;
+  if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded");
+  if (n < 0 || (n > 0 && (!rays || !out))) return fail(c, RT_E_INVALID, "bad ray batch");
+  if (n == 0) return RT_OK;
+  static_assert(sizeof(rt_probe) == 176, "rt_probe layout (trace.hip ProbeOut)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  DevBuf r, h;
+  int st = upload(c, r, rays, (size_t)n * 6 * sizeof(double));
+  if (!st) st = ensure(c, h, (size_t)n * sizeof(rt_probe));
+  if (!st) {
+    DScene S = c->scene;
+    S.time0 = S.time1 = 0.0;  // (book-2 ray time 0, like the oracle's or_probe_segment)
+    hipError_t e = launch_probe(S, c->mk_threads >= kTraceThreadsWide3, static_cast<const double*>(r.p), n, seed,
+                                sample, draw, h.p, c->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, h.p, (size_t)n * sizeof(rt_probe), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) st = fail(c, RT_E_HIP, "rt_probe_segment: %s", hipGetErrorString(e));
+  }
+  release(r);
+  release(h);
+  return st;
+}
+
 int rt_synchronize(rt_ctx* c) {
   if (!c) return RT_E_INVALID;
   HIP_TRY(c, hipSetDevice(c->device));
@@ -1735,38 +1773,66 @@ uint64_t call_key(const rt_ctx* c, const rt_camera* cam, const rt_render_params*
   return f.h;
 }
 
-// Every rank must render the same scene with the same call key: a 16-byte-per-rank all-gather of (scene
-// digest, key), read on the host.  All ranks see the same gathered words, so a mismatch fails on every rank
-// alike (RT_E_INVALID naming the first differing rank), and no collective of the frame is issued.  The
-// agreed key is cached on the communicator: a rank whose key equals it skips the exchange (no host round
-// trip in a steady-state loop of frames).  Every rank of a correct program changes its key in the same call
-// (a new scene on every rank, new arguments on every rank), so all ranks exchange together; a rank that
-// changes its key alone exchanges while the others go on to the frame's collectives, which RCCL cannot
-// match — the check turns a silently wrong frame into a stall in that misuse (shirley_rt.h).
+// The gathered words of one call: RT_OK, or RT_E_INVALID naming the first rank that differs from rank 0.
+int key_verdict(rt_ctx* c, const uint64_t* words, int world) {
+  int what = 0;
+  const int r = key_mismatch(words, world, &what);
+  if (r < 0) return RT_OK;
+  if (what == 0)
+    return fail(c, RT_E_INVALID, "scene mismatch across ranks: rank %d holds scene %016llx, rank 0 %016llx", r,
+                (unsigned long long)words[2 * r], (unsigned long long)words[0]);
+  return fail(c, RT_E_INVALID,
+              "render arguments differ across ranks (partition, sample range, samples, seed, max_depth, "
+              "sample_chunk or camera): rank %d key %016llx, rank 0 %016llx",
+              r, (unsigned long long)words[2 * r + 1], (unsigned long long)words[1]);
+}
+
+// Every rank must render the same scene with the same call key (keycheck.h states the rule).  Every call
+// all-gathers each rank's 16-byte (scene digest, key) on every rank — one collective sequence on all ranks
+// whatever their arguments — copies the gathered words into pinned host memory and checks them: at once
+// when this rank's key is new (or SHIRLEY_KEY_CHECK=sync), else at the next call (no host round trip in a
+// steady loop of frames).  A failed check leaves no frame collective issued by this rank.
 int check_call_key(rt_ctx* c, rt_comm* m, uint64_t key, hipStream_t s) {
-  if (m->verified && m->verified_key == key) return RT_OK;
-  const size_t bytes = (size_t)m->world * 2 * sizeof(uint64_t);
-  int st = ensure(c, c->digests, bytes + 2 * sizeof(uint64_t));
-  if (st) return st;
-  uint64_t* d = static_cast<uint64_t*>(c->digests.p);
-  const uint64_t mine[2] = {c->digest, key};
-  HIP_TRY(c, hipMemcpyAsync(d + 2 * m->world, mine, sizeof mine, hipMemcpyHostToDevice, s));
-  RCCL_TRY(c, rccl().AllGather(d + 2 * m->world, d, 2, ncclUint64, m->comm, s));
-  std::vector<uint64_t> all(2 * (size_t)m->world);
-  HIP_TRY(c, hipMemcpyAsync(all.data(), d, bytes, hipMemcpyDeviceToHost, s));
-  HIP_TRY(c, hipStreamSynchronize(s));
-  for (int r = 0; r < m->world; ++r)
-    if (all[2 * r] != all[0])
-      return fail(c, RT_E_INVALID, "scene mismatch across ranks: rank %d holds scene %016llx, rank 0 %016llx", r,
-                  (unsigned long long)all[2 * r], (unsigned long long)all[0]);
-  for (int r = 0; r < m->world; ++r)
-    if (all[2 * r + 1] != all[1])
-      return fail(c, RT_E_INVALID,
-                  "render arguments differ across ranks (partition, sample range, samples, seed, max_depth, "
-                  "sample_chunk or camera): rank %d key %016llx, rank 0 %016llx",
-                  r, (unsigned long long)all[2 * r + 1], (unsigned long long)all[1]);
-  m->verified = true;
-  m->verified_key = key;
+  const int W = m->world;
+  const size_t slot_words = 2 * (size_t)(W + 1);
+  int st;
+  if (!m->key_words) {
+    HIP_TRY(c, hipHostMalloc(reinterpret_cast<void**>(&m->key_words), 2 * slot_words * sizeof(uint64_t), 0));
+    for (hipEvent_t& e : m->key_ev) HIP_TRY(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  // the previous call's words: the deferred half of its check
+  if (m->ks.pending) {
+    m->ks.pending = false;
+    HIP_TRY(c, hipEventSynchronize(m->key_ev[m->key_pending]));
+    if ((st = key_verdict(c, m->key_words + m->key_pending * slot_words, W))) {
+      m->ks.verified = false;
+      return st;
+    }
+  }
+  if ((st = ensure(c, c->digests, 2 * slot_words * sizeof(uint64_t)))) return st;
+  const int slot = m->key_slot;
+  m->key_slot ^= 1;
+  uint64_t* hw = m->key_words + slot * slot_words;  // (this slot's last check was done: at most one pending)
+  uint64_t* dw = static_cast<uint64_t*>(c->digests.p) + slot * slot_words;
+  hw[2 * W] = c->digest;
+  hw[2 * W + 1] = key;
+  HIP_TRY(c, hipMemcpyAsync(dw + 2 * W, hw + 2 * W, 2 * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  RCCL_TRY(c, rccl().AllGather(dw + 2 * W, dw, 2, ncclUint64, m->comm, s));
+  HIP_TRY(c, hipMemcpyAsync(hw, dw, 2 * (size_t)W * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipEventRecord(m->key_ev[slot], s));
+  const char* e = getenv("SHIRLEY_KEY_CHECK");
+  if (key_check_now(m->ks, key, e && !strcmp(e, "sync"))) {
+    HIP_TRY(c, hipEventSynchronize(m->key_ev[slot]));
+    if ((st = key_verdict(c, hw, W))) {
+      m->ks.verified = false;
+      return st;
+    }
+    m->ks.verified = true;
+    m->ks.verified_key = key;
+  } else {
+    m->ks.pending = true;
+    m->key_pending = slot;
+  }
   return RT_OK;
 }
 
@@ -1809,10 +1875,11 @@ int rt_comm_init_rank(rt_ctx* c, const uint8_t id[RT_COMM_ID_BYTES], int32_t wor
 
 int rt_comm_destroy(rt_comm* m) {
   if (!m) return RT_OK;
-  if (m->comm && rccl().ok()) {
-    (void)hipSetDevice(m->device);
-    (void)rccl().CommDestroy(m->comm);
-  }
+  (void)hipSetDevice(m->device);
+  if (m->comm && rccl().ok()) (void)rccl().CommDestroy(m->comm);
+  for (hipEvent_t e : m->key_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (m->key_words) (void)hipHostFree(m->key_words);
   delete m;
   return RT_OK;
 }

@@ -1209,8 +1209,11 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
   const RayF rf = ray_f<typename Node4Sel<EXT>::T>(S, o, inv);
   const double a = len2(d);
   const Recip ra = recip(a);  // the sphere roots' divisor, shared (sphere_t_sure)
-  // the shared-reciprocal divisions' operand ranges: a (sphere roots) and every |d_i| (face planes, face_div)
-  const bool ra_ok = inv_ok && a >= 0x1p-300 && a <= 0x1p300 && rf.fast;
+  // the shared-reciprocal divisions' operand ranges: a (sphere roots) and every |d_i| (face planes, face_div),
+  // and t_min >= 0.001, which keeps an accepted face quotient's numerator >= 2^-310 (face_div's proof; a
+  // caller of rt_scene_hit_ex may pass a smaller t_min: those rays divide exactly like the reference).
+  // The megakernel's literal 0.001 folds the last test away.
+  const bool ra_ok = inv_ok && a >= 0x1p-300 && a <= 0x1p300 && rf.fast && t_min >= 0.001;
   float tmaxf = tmax_f32(t_best);
   int best = -1;
   int sp = 0;

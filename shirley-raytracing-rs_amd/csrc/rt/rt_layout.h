@@ -7,6 +7,8 @@
 
 #include <stdint.h>
 
+#include "plan.h"  // (unit window sizes)
+
 namespace rt {
 
 // Tile geometry: a wave (64 lanes) owns an 8x8 pixel tile of one sample chunk.
@@ -210,6 +212,10 @@ struct DWork {
   // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
   // segment, then steal from the next segments that still hold units
   uint32_t seg_len, n_segs;
+  // shared queue (n_segs == 0): units per atomic while more than q_tail units remain after the wave's
+  // previous window, kSegmentWindow after that (plan.h; read through work_const where a unit is taken)
+  uint32_t q_window, pad_q;
+  uint64_t q_tail;
 };
 
 // Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot
@@ -219,10 +225,7 @@ struct DCounters {
   unsigned long long pad[12];
 };
 constexpr int kCounterSlots = 64;
-// Work units a megakernel wave takes per queue atomic (a multiple of the wave size): kSegmentWindow from
-// a block's own segment, kQueueWindow from the one shared queue (plan.h).
-constexpr unsigned kSegmentWindow = 64;
-constexpr unsigned kQueueWindow = 256;
+// (work units a megakernel wave takes per queue atomic: kSegmentWindow / kQueueWindow, plan.h)
 // instrumented build: DCounters.pad slots of the megakernel's phase clocks (PH_STAMP in trace.hip) and
 // traversal step statistics
 enum : int {

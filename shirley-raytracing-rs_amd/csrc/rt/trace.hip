@@ -186,6 +186,7 @@ void trace_kernel(KParams P) {
       unsigned long long rank = __popcll(mask & lanemask_lt());
       unsigned long long avail = w_end - w_next;
       unsigned long long idx;
+      unsigned win = kSegmentWindow;  // units of the window taken below
       if (avail >= k) {
         idx = w_next + rank;
         w_next += k;
@@ -225,14 +226,31 @@ void trace_kernel(KParams P) {
           if (!found) break;
         }
         } else {  // one shared queue (short units: DWork.n_segs = 0)
+          // big windows while more than q_tail units remain, 64-unit windows for the pool's end (plan.h);
+          // the policy is read with scalar loads here, like the unit fetch.  The wave's own view of the
+          // counter (its previous window's end) is stale by the units every other wave took since — most
+          // for the slowest waves, whose big windows would make the frame's tail — so near the end the
+          // counter's current value decides (one atomic load per take).
+          KWork* kw = (KWork*)(uintptr_t)P.work_const;
+          asm volatile("" : "+s"(kw));
+          const unsigned long long tail = kw->q_tail;
+          unsigned long long left = W.n_units > w_end ? W.n_units - w_end : 0ull;
+          if (left <= 4ull * tail) {
+            unsigned long long cur = 0;
+            if (lane == 0) cur = __hip_atomic_load(P.unit_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cur = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(cur >> 32)) << 32) |
+                  (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)cur);
+            left = W.n_units > cur ? W.n_units - cur : 0ull;
+          }
+          win = left > tail ? kw->q_window : kSegmentWindow;
           nb = 0;
-          if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)kQueueWindow);
+          if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)win);
           nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
                (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
         }
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
-        w_end = nb + (W.n_segs != 0u ? kSegmentWindow : kQueueWindow);
+        w_end = nb + win;
         if (nb >= W.n_units) exhausted = true;
       }
       if (need && idx < W.n_units) {
@@ -573,6 +591,122 @@ __global__ __launch_bounds__(kHitThreads) void hit4_kernel(DScene S, const doubl
   out[i] = r;
 }
 
+// rt_probe_segment: one ray_color iteration (render.rs:30-46) per given ray through trace_kernel's own
+// steps 1, 3 and 4 for a lane that holds a path — the render traversal, the hit record, the material and
+// its texture leaf, the wave's marble and sampler, the one normalisation, shade_factor (or the sky) — on
+// the path key (seed, pixel = ray index, sample, draw).  Lanes past n take part in the wave-wide steps
+// idle, like a megakernel lane without a path.
+struct ProbeOut {
+  int32_t object, front_face, scattered, emits;
+  uint32_t draw;
+  int32_t pad;
+  double t, point[3], normal[3], emitted[3], attenuation[3], origin[3], direction[3];
+};
+static_assert(sizeof(ProbeOut) == 176, "ProbeOut is rt_probe (include/shirley_rt.h)");
+template <int MODE, bool EXT>
+__global__ __launch_bounds__(kHitThreads) void probe_kernel(DScene S, const double* __restrict__ rays, int n,
+                                                            uint64_t seed, uint32_t sample, uint32_t draw0,
+                                                            ProbeOut* __restrict__ out) {
+  extern __shared__ unsigned char lds_raw[];
+  const int tid = threadIdx.x;
+  typedef typename Node4Sel<EXT>::T N4;
+  N4* lds_nodes = reinterpret_cast<N4*>(lds_raw);
+  DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4));
+  const DPerlin* lds_perlin = (MODE == kSceneLds && S.n_lds_perlin > 0)
+                                  ? reinterpret_cast<const DPerlin*>(lds_prims + S.n_lds_prims)
+                                  : nullptr;
+  unsigned char* stk_base = lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4) +
+                            (MODE == kSceneLds ? (size_t)S.n_lds_prims * sizeof(DPrim) +
+                                                     (size_t)S.n_lds_perlin * sizeof(DPerlin)
+                                               : 0);
+  unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;
+  stage_nodes4<MODE>(S, lds_nodes, lds_prims);
+  const int i = blockIdx.x * kHitThreads + tid;
+  const bool active = i < n;
+  v3 o = V(0.0, 0.0, 0.0), d = V(1.0, 1.0, 1.0);
+  if (active) {
+    o = V(rays[i * 6 + 0], rays[i * 6 + 1], rays[i * 6 + 2]);
+    d = V(rays[i * 6 + 3], rays[i * 6 + 4], rays[i * 6 + 5]);
+  }
+  Rng rng{(uint32_t)i, sample, draw0, 0u, 0u};
+  if (draw0 & 1u) {  // an odd counter reads the odd half of block draw0 / 2 from the cache
+    uint64_t e0, e1;
+    philox_block(seed, rng.pixel, rng.sample, draw0 >> 1, e0, e1);
+    rng.c2 = (uint32_t)e1;
+    rng.c3 = (uint32_t)(e1 >> 32);
+  }
+  unsigned visits = 0, ptests = 0;
+#ifdef RT_PHASE_TIMING
+  unsigned long long steps = 0;
+#endif
+  // step 1 (trace_kernel): closest hit, record, material, texture leaf
+  bool hit = false, need_pn = false, need_r = false;
+  int prim = -1, face = -1, leaf = -1, mat = 0, ptab = 0, mk = -1;
+  double t_best = __builtin_inf(), psc = 0.0;
+  Hit h;
+  h.point = V(0.0, 0.0, 0.0);
+  h.normal = h.point;
+  h.t = h.u = h.v = 0.0;
+  h.front_face = false;
+  if (active) {
+    prim = traverse4<kHitThreads, MODE, EXT>(S, lds_nodes, lds_prims, o, d, 0.001, t_best, face, stk, rng, seed, visits,
+                                              ptests RT_STAT_ARG(steps));
+    if (prim >= 0) {
+      hit = true;
+      const DPrim pr = (MODE == kSceneLds) ? lds_prims[prim] : S.prims[prim];
+      hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
+      mat = pr.material;
+      mk = S.mats[mat].kind;
+      need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
+      if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
+        leaf = resolve_texture(S, S.mats[mat].tex, h.point);
+        const DTex& tx = S.texs[leaf];
+        if (tx.kind == RT_TEX_PERLIN) {
+          need_pn = true;
+          ptab = tx.table;
+          psc = tx.scale;
+        }
+      }
+    }
+  }
+  const bool ends = active && (!hit || mk == RT_MAT_DIFFUSE_LIGHT);
+  // step 3: the wave's marble values and draws
+  const double pn = lds_perlin ? marble_coop((LdsPerlin*)lds_perlin, need_pn, ptab, psc, h.point)
+                               : marble_coop(S.perlin, need_pn, ptab, psc, h.point);
+  const bool scat = active && !ends;
+  const int dk = (scat && need_r) ? kDrawSphere : (scat && mk == RT_MAT_DIELECTRIC) ? kDrawDiel : kDrawNone;
+  double jx = 0.0, jy = 0.0;
+  const v3 rs = draws_coop(rng, seed, dk, false, 0u, jx, jy);
+  const v3 un = unit_fast(!active ? V(1.0, 1.0, 1.0) : (scat && need_r && mk != RT_MAT_METAL) ? rs : d);
+  // step 4: emitted + scatter, or the sky
+  if (!active) return;
+  ProbeOut r{};
+  r.object = prim;
+  bool alive = false, has_emit = false;
+  v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
+  if (hit) {
+    const DMat m = S.mats[mat];
+    alive = shade_factor(S, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
+    r.front_face = h.front_face ? 1 : 0;
+    r.t = h.t;
+    r.point[0] = h.point.x; r.point[1] = h.point.y; r.point[2] = h.point.z;
+    r.normal[0] = h.normal.x; r.normal[1] = h.normal.y; r.normal[2] = h.normal.z;
+  } else {
+    emit = sky_unit(S, un);
+    has_emit = true;
+  }
+  r.scattered = alive ? 1 : 0;
+  r.emits = has_emit ? 1 : 0;
+  r.draw = rng.draw;
+  r.emitted[0] = emit.x; r.emitted[1] = emit.y; r.emitted[2] = emit.z;
+  if (alive) {
+    r.attenuation[0] = mul.x; r.attenuation[1] = mul.y; r.attenuation[2] = mul.z;
+    r.origin[0] = o.x; r.origin[1] = o.y; r.origin[2] = o.z;
+    r.direction[0] = d.x; r.direction[1] = d.y; r.direction[2] = d.z;
+  }
+  out[i] = r;
+}
+
 // ------------------------------------------------------------------------------------------
 // launch wrappers (called from rt_api.cpp)
 // ------------------------------------------------------------------------------------------
@@ -717,6 +851,42 @@ hipError_t launch_hit4(const DScene& S, bool wide, const double* rays, int n, do
     case kNodesLds: return launch_hit4_m<kNodesLds>(S, rays, n, t_min, t_max, o, blocks, stream);
     case kNodesGlobal: return launch_hit4_m<kNodesGlobal>(S, rays, n, t_min, t_max, o, blocks, stream);
     default: return launch_hit4_m<kNodesMixed>(S, rays, n, t_min, t_max, o, blocks, stream);
+  }
+}
+
+template <int MODE, bool EXT>
+static hipError_t launch_probe_1(const DScene& S, const double* rays, int n, uint64_t seed, uint32_t sample,
+                                 uint32_t draw, ProbeOut* o, int blocks, hipStream_t stream) {
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(EXT), MODE == kSceneLds ? S.n_lds_prims : 0,
+                                     MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads);
+  hipError_t e = hipFuncSetAttribute((const void*)probe_kernel<MODE, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((probe_kernel<MODE, EXT>), dim3(blocks), dim3(kHitThreads), lds, stream, S, rays, n, seed, sample,
+                     draw, o);
+  return hipGetLastError();
+}
+template <int MODE>
+static hipError_t launch_probe_m(const DScene& S, const double* rays, int n, uint64_t seed, uint32_t sample,
+                                 uint32_t draw, ProbeOut* o, int blocks, hipStream_t stream) {
+  return S.exts ? launch_probe_1<MODE, true>(S, rays, n, seed, sample, draw, o, blocks, stream)
+                : launch_probe_1<MODE, false>(S, rays, n, seed, sample, draw, o, blocks, stream);
+}
+
+// rt_probe_segment: the node / primitive placement the trace kernel uses (`wide`, as launch_hit4)
+hipError_t launch_probe(const DScene& S, bool wide, const double* rays, int n, uint64_t seed, uint32_t sample,
+                        uint32_t draw, void* out, hipStream_t stream) {
+  const int blocks = (n + kHitThreads - 1) / kHitThreads;
+  if (blocks == 0) return hipSuccess;
+  ProbeOut* o = static_cast<ProbeOut*>(out);
+  if (wide) {
+    if (S.n_lds_prims > 0) return launch_probe_m<kSceneLds>(S, rays, n, seed, sample, draw, o, blocks, stream);
+    return launch_probe_m<kNodesLds>(S, rays, n, seed, sample, draw, o, blocks, stream);
+  }
+  switch (node_mode4(S)) {
+    case kNodesLds: return launch_probe_m<kNodesLds>(S, rays, n, seed, sample, draw, o, blocks, stream);
+    case kNodesGlobal: return launch_probe_m<kNodesGlobal>(S, rays, n, seed, sample, draw, o, blocks, stream);
+    default: return launch_probe_m<kNodesMixed>(S, rays, n, seed, sample, draw, o, blocks, stream);
   }
 }
 

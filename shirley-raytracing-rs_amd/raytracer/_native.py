@@ -108,6 +108,12 @@ class rt_hit(C.Structure):
                 ("normal", _d3), ("u", C.c_double), ("v", C.c_double)]
 
 
+class rt_probe(C.Structure):
+    _fields_ = [("object", C.c_int32), ("front_face", C.c_int32), ("scattered", C.c_int32), ("emits", C.c_int32),
+                ("draw", C.c_uint32), ("pad", C.c_int32), ("t", C.c_double), ("point", _d3), ("normal", _d3),
+                ("emitted", _d3), ("attenuation", _d3), ("origin", _d3), ("direction", _d3)]
+
+
 class sh_camera_spec(C.Structure):
     _fields_ = [("width", C.c_int32), ("ratio_num", C.c_int32), ("ratio_den", C.c_int32),
                 ("vfov", C.c_double), ("focal_length", C.c_double), ("has_aperture", C.c_int32),
@@ -140,6 +146,8 @@ RT_SIGNATURES = {
     "rt_scene_hit": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.POINTER(rt_hit)]),
     "rt_scene_hit_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_double, C.c_double, C.c_int32,
                                   C.POINTER(rt_hit)]),
+    "rt_probe_segment": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_uint64, C.c_uint32, C.c_uint32,
+                                   C.POINTER(rt_probe)]),
     "rt_synchronize": (C.c_int, [C.c_void_p]),
     "rt_comm_unique_id": (C.c_int, [C.c_void_p]),
     "rt_comm_init_rank": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),

@@ -144,6 +144,16 @@ class Device:
         _check(self._h, code)
         return out[:len(r)]
 
+    def probe(self, rays: np.ndarray, seed: int, sample: int = 0, draw: int = 0):
+        """One iteration of ray_color's loop (render.rs:30-46) per ray through the megakernel's device code
+        (rt_probe_segment): ray i on the path key (seed, pixel = i, sample, draw) -> rt_probe array
+        (closest object, emitted / scatter of its material or the sky, the draw counter after it)."""
+        r = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        out = (N.rt_probe * max(1, len(r)))()
+        _check(self._h, N.rt_lib().rt_probe_segment(self._h, r.ctypes.data, len(r), int(seed), int(sample),
+                                                     int(draw), out))
+        return out[:len(r)]
+
     def synchronize(self):
         _check(self._h, N.rt_lib().rt_synchronize(self._h))
 

@@ -63,6 +63,9 @@ _SIGS = {
                                   C.c_void_p, C.POINTER(or_counters)]),
     "or_render_rows": (C.c_int32, [C.c_void_p, C.POINTER(N.rt_camera), C.POINTER(N.rt_render_params), C.c_int32,
                                    C.c_int32, C.c_int32, C.c_void_p, C.POINTER(or_counters)]),
+    "or_probe_segment": (None, [C.c_void_p, _d6, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                 C.POINTER(N.rt_probe)]),
+    "or_reflectance": (C.c_double, [C.c_double, C.c_double]),
     "or_tonemap": (None, [C.c_void_p, C.c_int32, C.c_int32, C.c_int32, C.c_void_p]),
 }
 
@@ -127,6 +130,12 @@ class OracleScene:
         if rc:
             raise RuntimeError("or_render_rows failed")
         return out, cnt
+
+    def probe(self, ray, seed, pixel, sample=0, draw=0):
+        """One ray_color loop iteration for `ray` on the path key (seed, pixel, sample, draw): rt_probe."""
+        out = N.rt_probe()
+        lib().or_probe_segment(self.h, d6(ray), int(seed), int(pixel), int(sample), int(draw), C.byref(out))
+        return out
 
     def sample(self, cam, params, px, py, s):
         out = (C.c_double * 3)()

@@ -11,9 +11,11 @@ at exactly the same t, which changes one whole path.  One rule for every GPU-vs-
     render.rs:58-69),
   * every channel within TOL = 1e-10 * spp absolute of the oracle, except at most 0.1 % of pixels
     (PARITY_OUTLIERS: a flipped path changes one sample by up to the path's radiance).
-One stated exception: BASELINE config 5's band (CFG5_EXACT below, with its reason).  Measured fractions
-of every comparison: profiles/r04/parity_fractions*.jsonl (SHIRLEY_PARITY_LOG); each sits above its
-gate by at least the margin stated in DESIGN.md §2.
+One stated exception: BASELINE config 5's band (CFG5_EXACT below, with its reason).  On top of that rule,
+each comparison has its own floor (EXACT_FLOOR): its measured fraction in profiles/r04/parity_fractions.jsonl
+(SHIRLEY_PARITY_LOG) minus one channel in a thousand, capped at 0.9995 — so a scene measured bit-identical
+(1.0: Cornell, earth, demo, the config bands 3 and 4) fails on a systematic 1-ulp slip that touches more
+than 0.05 % of its channels, which the uniform 0.99 would let through.
 The trace engines (RT_ENGINE_MEGAKERNEL, RT_ENGINE_WAVEFRONT, RT_ENGINE_SPLIT) run the same binary64
 code on the same counter-RNG streams, so their frames must be bit-identical to each other: the
 megakernel (the engine the product runs) carries every test; each other engine keeps one smoke parity
@@ -34,6 +36,24 @@ ENGINES = ["megakernel"]  # the engine of every test below (RT_ENGINE_AUTO picks
 OTHER_ENGINES = ["wavefront", "split"]  # one smoke parity test each (slower engines)
 PARITY_EXACT = 0.99    # bit-identical channel fraction, every comparison
 PARITY_OUTLIERS = 0.001  # fraction of pixels allowed beyond 1e-10 * spp
+# Per-comparison floors of the bit-identical fraction: min(0.9995, measured - 0.001), from the round-4
+# calibration (profiles/r04/parity_fractions.jsonl); never below PARITY_EXACT (exact_floor).
+EXACT_FLOOR = {
+    # test_render_matches_oracle / test_other_engine_matches_oracle_and_megakernel (48- / 40-wide, 8 spp)
+    "random": 0.99566, "random-night": 0.9995, "demo": 0.9995, "perlin": 0.99386, "earth": 0.9995,
+    "box-light": 0.99746, "cornell": 0.9995, "final:6:60": 0.99838, "final": 0.9995,
+    # test_render_matches_golden (32 x 32 @ 8 spp)
+    "golden:random": 0.99437, "golden:cornell": 0.9995, "golden:earth": 0.9995, "golden:final:4:30": 0.9995,
+    # test_config_settings_band_matches_oracle (cfg5: its own exception, CFG5_EXACT)
+    "cfg1": 0.99451, "cfg3": 0.9995, "cfg3_ground": 0.9995, "cfg4": 0.9995, "cfg4_light": 0.9995,
+    "cfg5": 0.98021,
+    "spheres": 0.9995, "final_world8": 0.99873,
+}
+
+
+def exact_floor(key, base=PARITY_EXACT):
+    """The bit-identical fraction a comparison must reach: its calibrated floor, never below the rule."""
+    return max(base, EXACT_FLOOR.get(key, base))
 ENGINE_ID = {"megakernel": 1, "wavefront": 2, "split": 3}
 # RT_ENGINE_SPLIT serves reference scenes whose whole scene fits in LDS; book-2 scenes fall back to
 # the megakernel (rt_counters.engine reports the engine that ran)
@@ -88,7 +108,7 @@ def test_render_matches_oracle(gpu, name, width, aspect):
     for engine in ENGINES:
         img = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp,
                                                 engine=engine))
-        check_parity(img, ora, spp)
+        check_parity(img, ora, spp, frac_exact=exact_floor(name))
         cnt = gpu.counters()
         assert engine_ran(cnt, engine, name)
         assert cnt.samples == cam.image_width * cam.image_height * spp == ocnt.samples
@@ -98,7 +118,8 @@ def test_render_matches_oracle(gpu, name, width, aspect):
 
 
 @pytest.mark.parametrize("engine", OTHER_ENGINES)
-@pytest.mark.parametrize("name,width,aspect", [("random", 48, "std16x9"), ("cornell", 40, "square")])
+@pytest.mark.parametrize("name,width,aspect", [("random", 48, "std16x9"), ("cornell", 40, "square"),
+                                               ("perlin", 48, "std16x9"), ("final:6:60", 40, "square")])
 def test_other_engine_matches_oracle_and_megakernel(gpu, engine, name, width, aspect):
     """The smoke parity test of each non-default engine: the oracle's tolerance, and the megakernel's
     frame bit for bit (the same device functions on the same streams)."""
@@ -110,7 +131,7 @@ def test_other_engine_matches_oracle_and_megakernel(gpu, engine, name, width, as
     s = dict(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp)
     img = gpu.render(cam, rt.RenderSettings(**s, engine=engine))
     assert engine_ran(gpu.counters(), engine, name)
-    check_parity(img, ora, spp)
+    check_parity(img, ora, spp, frac_exact=exact_floor(name))
     assert np.array_equal(img, gpu.render(cam, rt.RenderSettings(**s, engine="megakernel")))
 
 
@@ -124,7 +145,7 @@ def test_render_matches_golden(gpu, name, aspect):
     gpu.upload(rt.SceneBuilder.builtin(name, SEED).finalize(SEED))
     img = gpu.render(rt.scene_camera(name, 32, aspect), rt.RenderSettings(samples=8, max_reflect=50, seed=SEED,
                                                                           sample_chunk=8))
-    check_parity(img, gold[key], 8)
+    check_parity(img, gold[key], 8, frac_exact=exact_floor("golden:" + name))
 
 
 def test_hit_queries_match_golden(gpu):
@@ -227,7 +248,7 @@ def test_large_scene_mixed_lds_matches_oracle(gpu, engine):
     for bvh in ("reference", "sah"):
         img = gpu.upload(scene, bvh).render(cam, rt.RenderSettings(engine=engine, samples=spp, seed=SEED, sample_chunk=spp))
         ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED))
-        check_parity(img, ora, spp)
+        check_parity(img, ora, spp, frac_exact=exact_floor("spheres"))
 
 
 def test_hit_queries_match_oracle(gpu):
@@ -537,7 +558,7 @@ def test_config_settings_band_matches_oracle(gpu, key, name, width, aspect, spp,
     assert np.all(np.abs(band - inorder) <= 1e-12 * np.abs(inorder))
     ora, cnt = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), r0, r1, threads=16)
     assert cnt.samples == cam.image_width * rows * spp
-    check_parity(inorder, ora, spp, frac_exact=CFG5_EXACT if key == "cfg5" else PARITY_EXACT)
+    check_parity(inorder, ora, spp, frac_exact=exact_floor(key, CFG5_EXACT if key == "cfg5" else PARITY_EXACT))
 
 
 def test_max_depth_zero_partial_units(gpu):
@@ -580,7 +601,7 @@ def test_final_scene_tile_sharded_world8(gpu):
     gpu.synchronize()
     assert np.array_equal(accum.cpu().numpy(), full)
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
-    check_parity(full, ora, spp)
+    check_parity(full, ora, spp, frac_exact=exact_floor("final_world8"))
 
 
 @pytest.mark.parametrize("bvh", ["reference", "sah"])
@@ -595,4 +616,4 @@ def test_gen_spheres_side11_matches_oracle(gpu, bvh):
     assert gpu.stats().wide_block == 0
     img = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
-    check_parity(img, ora, spp)
+    check_parity(img, ora, spp, frac_exact=exact_floor("spheres"))

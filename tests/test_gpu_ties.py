@@ -1,0 +1,126 @@
+"""Exact ties in t: two primitives hit at the same binary64 t.
+
+The reference accepts a hit at t == the running closest t (sphere.rs:40-45 rejects only `t_max < root`,
+rect.rs:58 only `t > t_max`), so the tied primitive tested LAST wins — provided its bounding box passes
+`hit2` (aabb.rs:62-79), whose `t_max <= t_min` test is strict, at t_max = the tie.  The order differs:
+  * reference: bbox_tree.rs:56-91 pops rhs before lhs, so of two sibling leaves the lhs is tested last;
+  * this build (rt_device.h leaf_tests4): a 4-wide node's hit leaves are tested spheres first (in child-slot
+    order: the collapse keeps a binary node's lhs before its rhs), then RectBoxes, then rects — so of two
+    sibling spheres the rhs wins, and a rect wins over a RectBox face it coincides with.
+No reference scene produces a tie (the random scene's coat, y in [-0.01, 0], lies 0.01 above its lower
+surface at y = -0.02: scenes.rs:251-279; the Cornell walls meet only at edges).  Constructed here: two
+coincident spheres, and an xz_rect coplanar with a RectBox's top face.  The tests pin the device's choice,
+check that its hit record (t, point, normal) is the reference's, and measure how far a frame departs from
+the oracle's (reference-order) frame — recorded with SHIRLEY_PARITY_LOG and in DESIGN.md §8."""
+import ctypes as C
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import raytracer as rt
+from raytracer import _native as N
+from test_scatter_kat import KatScene
+
+pytestmark = pytest.mark.gpu
+SEED = 0x5EED
+RED = {"kind": N.RT_TEX_SOLID, "color": (0.9, 0.1, 0.1)}
+GREEN = {"kind": N.RT_TEX_SOLID, "color": (0.1, 0.9, 0.1)}
+MATS = [(N.RT_MAT_LAMBERTIAN, 0, (0, 0, 0), 0.0), (N.RT_MAT_LAMBERTIAN, 1, (0, 0, 0), 0.0)]
+
+
+def _root_children(scene):
+    """(lhs leaf object, rhs leaf object) of the reference builder's root (the tree both sides build)."""
+    n = C.c_int32(0)
+    assert N.rt_lib().rt_bvh_build_host(scene.desc_ptr, N.RT_BVH_REFERENCE, C.byref(n), None, None) == 0
+    arr = (N.rt_bvh_node * n.value)()
+    root = C.c_int32(0)
+    assert N.rt_lib().rt_bvh_build_host(scene.desc_ptr, N.RT_BVH_REFERENCE, C.byref(n), arr, C.byref(root)) == 0
+    r = arr[root.value]
+    return arr[r.lhs].leaf, arr[r.rhs].leaf
+
+
+def _log(name, **kv):
+    path = os.environ.get("SHIRLEY_PARITY_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"test": name, **kv}) + "\n")
+
+
+def _frame_departure(gpu, scene, cam, spp=4):
+    img = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
+    ora, _ = O.OracleScene(scene.desc).render(cam, O.params(spp, 50, SEED))
+    bad = np.any(np.abs(img - ora) > 1e-10 * spp, axis=-1)
+    return float(bad.mean()), float(np.mean(img == ora))
+
+
+def _upload(gpu, scene):
+    rt.Device.upload(gpu, type("S", (), {"desc_ptr": scene.desc_ptr})())
+
+
+def test_coincident_spheres_tie(gpu):
+    scene = KatScene([(N.RT_GEOM_SPHERE, 0, [0.0, 0.0, -3.0, 1.0]), (N.RT_GEOM_SPHERE, 1, [0.0, 0.0, -3.0, 1.0])],
+                     MATS, [RED, GREEN])
+    lhs, rhs = _root_children(scene)
+    assert {lhs, rhs} == {0, 1}
+    _upload(gpu, scene)
+    osc = O.OracleScene(scene.desc)
+    rng = np.random.default_rng(11)
+    # rays from around (0, 0, 2) at the sphere, off the axes (the hit point strictly inside the box's faces)
+    tgt = np.array([0.0, 0.0, -3.0]) + rng.uniform(-0.5, 0.5, size=(256, 3))
+    org = np.array([0.3, 0.2, 2.0]) + rng.uniform(-0.5, 0.5, size=(256, 3))
+    rays = np.hstack([org, tgt - org])
+    dev = gpu.hit(rays, 0.001, float("inf"), traversal="render")
+    for i, ray in enumerate(rays):
+        h = osc.hit(ray)
+        g = dev[i]
+        assert h.hit and h.object == lhs  # the reference: lhs tested last
+        assert g.object == rhs            # this build: the higher child slot tested last
+        assert (g.t, list(g.point), list(g.normal), g.front_face) == (h.t, list(h.point), list(h.normal),
+                                                                       h.front_face)
+    # the frame: the sphere shows the other material wherever it is seen first-hand
+    cam = rt.CameraBuilder(width=32, aspect_ratio=(1, 1), vfov=40.0).build(rt.CameraPosition((0.0, 0.0, 2.0),
+                                                                                             (0.0, 0.0, -3.0)))
+    dep, exact = _frame_departure(gpu, scene, cam)
+    _log("ties:coincident_spheres", departure_px=dep, exact=exact)
+    assert 0.05 < dep < 0.6  # the visible sphere (~25 % of the frame) and its reflections
+
+
+def test_rect_coplanar_with_rectbox_face_tie(gpu):
+    # RectBox [-1, 1] x [-1, 0] x [-4, -2] and xz_rect [-1, 1] x [-4, -2] at y = 0: its top face, exactly
+    for order in ("box_first", "rect_first"):
+        box = (N.RT_GEOM_RECT_BOX, 0, [-1.0, -1.0, -4.0, 1.0, 0.0, -2.0])
+        rect = (N.RT_GEOM_RECT_XZ, 1, [-1.0, 1.0, -4.0, -2.0, 0.0])
+        objs = [box, rect] if order == "box_first" else [rect, box]
+        mats = MATS if order == "box_first" else MATS
+        scene = KatScene(objs, mats, [RED, GREEN])
+        rect_id = 1 if order == "box_first" else 0
+        _upload(gpu, scene)
+        osc = O.OracleScene(scene.desc)
+        rng = np.random.default_rng(12)
+        tgt = np.column_stack([rng.uniform(-0.9, 0.9, 256), np.zeros(256), rng.uniform(-3.9, -2.1, 256)])
+        org = tgt + np.column_stack([rng.uniform(-1, 1, 256), rng.uniform(0.5, 3, 256), rng.uniform(-1, 1, 256)])
+        org[:32, 0], org[:32, 2] = tgt[:32, 0], tgt[:32, 2]  # 32 vertical rays (1/d exact: the reference's rect wins)
+        rays = np.hstack([org, tgt - org])
+        dev = gpu.hit(rays, 0.001, float("inf"), traversal="render")
+        n_ref_rect = 0
+        for i, ray in enumerate(rays):
+            h = osc.hit(ray)
+            g = dev[i]
+            assert h.hit and g.object == rect_id, (order, i)  # this build: rects after RectBoxes, rect wins
+            assert (g.t, list(g.point), list(g.normal)) == (h.t, list(h.point), list(h.normal))
+            n_ref_rect += h.object == rect_id
+            if i < 32:
+                # vertical rays: the box's slab entry at y = 0 is exactly the tie, and hit2's strict
+                # `t_max <= t_min` rejects the box whichever is tested last: the reference's rect wins too
+                assert h.object == rect_id
+        _log(f"ties:rect_on_rectbox_face:{order}", reference_rect_fraction=n_ref_rect / len(rays))
+        cam = rt.CameraBuilder(width=32, aspect_ratio=(1, 1), vfov=40.0).build(
+            rt.CameraPosition((0.0, 3.0, 0.5), (0.0, 0.0, -3.0)))
+        dep, exact = _frame_departure(gpu, scene, cam)
+        _log(f"ties:rect_on_rectbox_face_frame:{order}", departure_px=dep, exact=exact)
+        # where the reference also picks the rect (every vertical-ish ray whose 1/d entry rounds at or
+        # past the tie) the frames agree; the rest of the face departs
+        assert dep <= 0.6
