@@ -35,8 +35,8 @@ struct SamplePlan {
   int passes = 0;
   long long partial_bytes = 0;  // scratch of one pass
   bool segments = false;  // megakernel per-block unit segments (units of >= 4 samples)
-  // shared queue (segments off): a wave takes queue_window units per atomic while more than queue_tail
-  // units remain after its last window, kSegmentWindow after that
+  // shared queue (segments off): the pool's units but its last queue_tail go in queue_window-unit
+  // windows, those in kSegmentWindow-unit windows (bulk_end)
   unsigned queue_window = kQueueWindow;
   unsigned long long queue_tail = 0;
   bool ok = true;        // false: a pass cannot index one chunk of the frame in 32 bits
@@ -80,10 +80,10 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   // 24.5 -> 23.4 ms with 256-unit windows (512: 23.8, 1024: 25.2; with segments 128 / 256 cost the
   // headline 0.4 / 1.8 %), profiles/r04/shard_scan/.
   P.segments = engine == RT_ENGINE_MEGAKERNEL && chunk >= 4;
-  // The shared queue's windows shrink for the pool's end (guided self-scheduling): a wave's last window
-  // decides when it finishes, and 256 units are 4 per lane — on a small frame (cfg1 400x225 @ 50: 17
-  // units per lane) a ragged end of up to 4 units per lane.  So a wave takes 256-unit windows while more
-  // than one round of them (256 units per resident wave) remains, and 64-unit windows after that.
+  // The shared queue's windows shrink for the pool's end: a wave's last window decides when it finishes,
+  // and 256 units are 4 per lane — on a small frame (cfg1 400x225 @ 50: 17 units per lane) a ragged end
+  // of up to 4 units per lane.  So the pool's last round of 256-unit windows (256 units per resident
+  // wave) is served in 64-unit windows from a second counter (bulk_end below; trace.hip).
   P.queue_window = kQueueWindow;
   P.queue_tail = (unsigned long long)std::max(1LL, lanes / 64) * kQueueWindow;
 
@@ -103,6 +103,14 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   P.per_pass = (P.n_chunks + P.passes - 1) / P.passes;  // even passes
   P.partial_bytes = std::max<long long>(1, n_pix * P.per_pass * 3) * (long long)sizeof(double);
   return P;
+}
+
+// The shared queue's bulk: units [0, bulk_end) go in `window`-unit windows, the rest in 64-unit windows.
+// A multiple of the window (a bulk window never straddles into the tail), and 0 when the pool holds no
+// more than the tail.
+inline unsigned long long bulk_end(unsigned long long n_units, unsigned long long tail, unsigned window) {
+  const unsigned long long w = std::max(1u, window);
+  return n_units > tail ? (n_units - tail) / w * w : 0ull;
 }
 
 }  // namespace rt

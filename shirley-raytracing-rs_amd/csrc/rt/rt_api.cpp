@@ -105,6 +105,7 @@ struct rt_ctx {
   int n_perlin = 0;
   // per-render scratch
   DevBuf partial, accum, counters, unit_counter, kcam;
+  DevBuf shutter0;  // {0, 0}: the shutter of rt_scene_hit / rt_probe_segment queries (DScene.shutter)
   DevBuf wf_pool, wf_iters;          // path slots (SoA) + texture queue; per-iteration counters ring
   uint32_t* wf_host = nullptr;       // pinned readback of the retired-slot count, one word per batch
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
@@ -114,9 +115,7 @@ struct rt_ctx {
   int last_engine = 0, last_iters = 0, last_timing = 0, last_chunk = 0, last_n_chunks = 0, last_passes = 0;
   uint64_t last_slots = 0, last_scratch = 0;
   std::vector<hipEvent_t> pass_ev;   // before / after the trace launch of each sample pass
-  DCamera host_cam{};
-  DScene host_scene{};                // host sources of the device copies (KParams.cam_const / work_const)
-  std::vector<DWork> host_work;
+  std::vector<KBlock> host_blocks;    // host sources of the device KBlocks (KParams.kconst)
   uint64_t digest = 0;               // rt_scene_digest of the uploaded scene
   uint64_t host_samples = 0;  // samples of a frame served without a trace kernel (max_depth == 0)
   double lap_ms[3] = {0, 0, 0};
@@ -768,6 +767,7 @@ int run_wavefront(rt_ctx* c, const KParams& kp, bool timing, hipStream_t s) {
   P.scene = c->wf_scene;
   P.scene.time0 = kp.scene.time0;
   P.scene.time1 = kp.scene.time1;
+  P.scene.shutter = kp.scene.shutter;  // (the call's shutter, in the pass's KBlock)
   P.cam = kp.cam;
   P.work = kp.work;
   wf_carve(c->wf_pool.p, n, P);
@@ -934,23 +934,17 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
   kp.partial = static_cast<double*>(c->partial.p);
   kp.counters = static_cast<DCounters*>(c->counters.p);
 
-  // device copies of the camera, the scene record and each pass's work descriptor (KParams.cam_const /
-  // scene_const / work_const), 16-B aligned; their host sources stay alive in the ctx until the next call
-  constexpr size_t kCamBytes = (sizeof(DCamera) + 15) / 16 * 16, kSceneBytes = (sizeof(DScene) + 15) / 16 * 16;
-  st = ensure(c, c->kcam, kCamBytes + kSceneBytes + (size_t)passes * sizeof(DWork));
+  // the megakernel's per-pass KBlock (KParams.kconst): device copies of the camera, the scene record, the
+  // pass's work descriptor and the output / queue / statistics pointers; their host sources stay alive in
+  // the ctx until the next call
+  st = ensure(c, c->kcam, (size_t)passes * sizeof(KBlock));
   if (st) return st;
-  c->host_cam = kp.cam;
-  c->host_scene = kp.scene;
-  c->host_work.assign(passes, DWork{});
-  HIP_TRY(c, hipMemcpyAsync(c->kcam.p, &c->host_cam, sizeof(DCamera), hipMemcpyHostToDevice, s));
-  HIP_TRY(c, hipMemcpyAsync(static_cast<char*>(c->kcam.p) + kCamBytes, &c->host_scene, sizeof(DScene),
-                            hipMemcpyHostToDevice, s));
-  kp.cam_const = (uint64_t)(uintptr_t)c->kcam.p;
-  kp.scene_const = (uint64_t)(uintptr_t)(static_cast<char*>(c->kcam.p) + kCamBytes);
-
+  // every kernel of the call reads the shutter from pass 0's device copy of the scene record
+  kp.scene.shutter = &static_cast<KBlock*>(c->kcam.p)->scene.time0;
+  c->host_blocks.assign(passes, KBlock{});
   const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
   {
-    const size_t bytes = std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t));
+    const size_t bytes = std::max<size_t>(128, (size_t)nseg * sizeof(uint32_t));  // (>= the tail counter's line)
     st = ensure(c, c->unit_counter, bytes);
     if (st) return st;
     kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
@@ -1006,17 +1000,24 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     w.n_segs = plan.segments ? (uint32_t)nseg : 0u;
     w.seg_len = (uint32_t)std::max<uint64_t>(kSegmentWindow, (per + kSegmentWindow - 1) / kSegmentWindow * kSegmentWindow);
     w.q_window = plan.queue_window;
-    w.q_tail = plan.queue_tail;
-    if (const char* e = getenv("SHIRLEY_WINDOW"))  // (tuning: the shared queue's big window, units)
+    uint64_t tail = plan.queue_tail;
+    if (const char* e = getenv("SHIRLEY_WINDOW"))  // (tuning: the shared queue's bulk window, units)
       w.q_window = (uint32_t)std::max(1, atoi(e) / kWave) * (uint32_t)kWave;
-    if (const char* e = getenv("SHIRLEY_QUEUE_TAIL"))  // (tuning: units left below which windows are 64)
-      w.q_tail = (uint64_t)std::max(0LL, atoll(e));
+    if (const char* e = getenv("SHIRLEY_QUEUE_TAIL"))  // (tuning: units of the tail served in 64-unit windows)
+      tail = (uint64_t)std::max(0LL, atoll(e));
+    w.q_bulk_end = bulk_end(w.n_units, tail, w.q_window);
     // the device copy is taken after every field is set (the kernel may read any of them)
-    c->host_work[k] = w;
-    void* kwork = static_cast<char*>(c->kcam.p) + kCamBytes + kSceneBytes + (size_t)k * sizeof(DWork);
-    HIP_TRY(c, hipMemcpyAsync(kwork, &c->host_work[k], sizeof(DWork), hipMemcpyHostToDevice, s));
-    kp.work_const = (uint64_t)(uintptr_t)kwork;
-    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t)), s));
+    KBlock& kb = c->host_blocks[k];
+    kb.cam = kp.cam;
+    kb.scene = kp.scene;
+    kb.work = w;
+    kb.partial = kp.partial;
+    kb.unit_counter = kp.unit_counter;
+    kb.counters = kp.counters;
+    void* kdev = static_cast<KBlock*>(c->kcam.p) + k;
+    HIP_TRY(c, hipMemcpyAsync(kdev, &kb, sizeof(KBlock), hipMemcpyHostToDevice, s));
+    kp.kconst = (uint64_t)(uintptr_t)kdev;
+    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(128, (size_t)nseg * sizeof(uint32_t)), s));
     HIP_TRY(c, hipEventRecord(c->pass_ev[2 * k], s));
     if (engine == RT_ENGINE_WAVEFRONT) {
       st = run_wavefront(c, kp, timing, s);
@@ -1085,7 +1086,7 @@ int rt_destroy(rt_ctx* c) {
   if (!c) return RT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->texels, &c->exts, &c->partial, &c->kcam,
+  for (DevBuf* b : {&c->nodes, &c->nodes4, &c->prims, &c->mats, &c->texs, &c->perlin, &c->texels, &c->exts, &c->partial, &c->kcam, &c->shutter0,
                     &c->accum, &c->counters, &c->unit_counter, &c->wf_pool, &c->wf_iters, &c->packed, &c->gathered,
                     &c->parts, &c->band, &c->digests})
     release(*b);
@@ -1272,6 +1273,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   S.perlin = static_cast<const DPerlin*>(c->perlin.p);
   S.exts = exts.empty() ? nullptr : static_cast<const DExt*>(c->exts.p);
   S.time0 = S.time1 = 0.0;  // the shutter comes with each render call's camera
+  if ((st = ensure(c, c->shutter0, 2 * sizeof(double)))) return st;
+  HIP_TRY(c, hipMemset(c->shutter0.p, 0, 2 * sizeof(double)));
+  S.shutter = static_cast<const double*>(c->shutter0.p);
   S.n_nodes = (int32_t)nodes.size();
   S.n_prims = d->n_objects;
   int32_t depth = tree_branch_depth(tree);

@@ -388,9 +388,12 @@ __device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, 
 __device__ __forceinline__ const DExt& prim_ext(const DScene& S, const DPrim& pr) {
   return S.exts[pr.kind >> kPrimExtShift];
 }
-// camera.h get_ray (book 2): time = random_double(time0, time1), drawn from the path's time stream
-__device__ __forceinline__ double ray_time(double time0, double time1, uint32_t pixel, uint32_t sample,
-                                           uint64_t seed) {
+// camera.h get_ray (book 2): time = random_double(time0, time1), drawn from the path's time stream; the
+// shutter {time0, time1} read here (DScene.shutter), not held across the caller's loop
+__device__ __forceinline__ double ray_time(const double* shutter, uint32_t pixel, uint32_t sample, uint64_t seed) {
+  const double* sh = shutter;
+  asm volatile("" : "+s"(sh));
+  const double time0 = sh[0], time1 = sh[1];
   return time0 + (time1 - time0) * side_draw(seed, 0u, sample, pixel, kStreamTime);
 }
 // moving_sphere.h center(time) = center0 + ((time - time0) / (time1 - time0)) * (center1 - center0)
@@ -436,13 +439,13 @@ struct ExtHit {
   int face;
   int hit;
 };
-__device__ __forceinline__ ExtHit ext_t(const DExt* exts, double time0, double time1, const DPrim pr, int prim, v3 o,
+__device__ __forceinline__ ExtHit ext_t(const DExt* exts, const double* shutter, const DPrim pr, int prim, v3 o,
                                      v3 d, double t_min, double t_max, uint32_t pixel, uint32_t sample,
                                      uint32_t draw, uint64_t seed) {
   ExtHit r{0.0, -1, 0};
   const DExt& e = exts[pr.kind >> kPrimExtShift];
   const int32_t kind = pr.kind, base = kind & kPrimBaseMask;
-  const double tm = base == kPrimMovingSphere ? ray_time(time0, time1, pixel, sample, seed) : 0.0;
+  const double tm = base == kPrimMovingSphere ? ray_time(shutter, pixel, sample, seed) : 0.0;
   to_object(e, kind, o, d);
   if (!(kind & kPrimMedium)) {
     r.hit = base_t(pr, e, base, o, d, tm, t_min, t_max, r.t, r.face) ? 1 : 0;
@@ -489,7 +492,7 @@ __device__ __forceinline__ ExtHit ext_t(const DExt* exts, double time0, double t
 }
 __device__ __forceinline__ bool ext_hit_t(const DScene& S, const DPrim& pr, int prim, v3 o, v3 d, double t_min,
                                           double t_max, const Rng& rk, uint64_t seed, double& t, int& face) {
-  const ExtHit r = ext_t(S.exts, S.time0, S.time1, pr, prim, o, d, t_min, t_max, rk.pixel, rk.sample, rk.draw, seed);
+  const ExtHit r = ext_t(S.exts, S.shutter, pr, prim, o, d, t_min, t_max, rk.pixel, rk.sample, rk.draw, seed);
   if (r.hit) {
     t = r.t;
     face = r.face;
@@ -583,7 +586,7 @@ __device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 
 // (a medium's: point r.at(t), normal (1, 0, 0), front face — constant_medium.h), then RotateY::hit
 // and Translate::hit map point and normal back to the world (front_face kept from the object frame,
 // as in the books' current edition).
-__device__ __forceinline__ Hit ext_record(const DExt* exts, double time0, double time1, const DPrim pr, int face, v3 o,
+__device__ __forceinline__ Hit ext_record(const DExt* exts, const double* shutter, const DPrim pr, int face, v3 o,
                                        v3 d, double t, uint32_t pixel, uint32_t sample, uint64_t seed) {
   Hit h;
   const DExt& e = exts[pr.kind >> kPrimExtShift];
@@ -596,7 +599,7 @@ __device__ __forceinline__ Hit ext_record(const DExt* exts, double time0, double
     h.front_face = true;
     h.u = h.v = 0.0;
   } else if (base == kPrimMovingSphere) {
-    const v3 c = moving_center(pr, e, ray_time(time0, time1, pixel, sample, seed));
+    const v3 c = moving_center(pr, e, ray_time(shutter, pixel, sample, seed));
     h.t = t;
     h.point = o + scale(d, t);
     const v3 n = scale(h.point - c, pr.p[4]);  // p[4] = 1.0 / r (host)
@@ -620,7 +623,7 @@ __device__ __forceinline__ Hit ext_record(const DExt* exts, double time0, double
 template <bool WANT_UV, bool EXT>
 __device__ __forceinline__ void hit_record(const DScene& S, const DPrim& pr, int face, v3 o, v3 d, double t,
                                            const Rng& rk, uint64_t seed, Hit& h) {
-  if (EXT && (pr.kind & kPrimExt)) h = ext_record(S.exts, S.time0, S.time1, pr, face, o, d, t, rk.pixel, rk.sample, seed);
+  if (EXT && (pr.kind & kPrimExt)) h = ext_record(S.exts, S.shutter, pr, face, o, d, t, rk.pixel, rk.sample, seed);
   else prim_record<WANT_UV>(pr, face, o, d, t, h);
 }
 
@@ -1034,6 +1037,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     // primitive is re-read for it, so no copy of c, r is held across the sphere test.
     bool sure;
     if (!sphere_t_sure(pr.p, o, d, ra, ra_ok, t_min, t_best, t, sure)) continue;
+#ifdef RT_SURE_LDS_ONLY  // (A/B: the sure-pass only where the scene is LDS-resident)
+    if (MODE != kSceneLds) sure = false;
+#endif
     if (!sure) {
       const DPrim* pp = &pr;
       asm volatile("" : "+v"(pp));
@@ -1707,6 +1713,14 @@ __device__ __forceinline__ v3 draws_coop(Rng& r, uint64_t seed, int kind, bool l
 typedef __attribute__((address_space(4))) const DCamera KCamera;
 typedef __attribute__((address_space(4))) const DWork KWork;
 typedef __attribute__((address_space(4))) const DScene KScene;
+typedef __attribute__((address_space(4))) const KBlock KBlk;
+// the pass's KBlock behind an opaque copy of its address (the empty asm keeps the scalar loads from
+// being hoisted out of the megakernel's loop)
+__device__ __forceinline__ KBlk* kblock(uint64_t a) {
+  KBlk* kb = (KBlk*)(uintptr_t)a;
+  asm volatile("" : "+s"(kb));
+  return kb;
+}
 // x / n for the camera's jittered pixel coordinate x in [0, n], n = width or height <= 65536, with
 // r = RN(1 / n) from the host: q0 = x r is within an ulp of x / n, and one correction step with the
 // correctly rounded reciprocal gives the correctly rounded quotient (Markstein, IBM J. Res. Dev. 34,

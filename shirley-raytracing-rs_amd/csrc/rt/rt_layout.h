@@ -162,7 +162,9 @@ struct DScene {
   int32_t sky;
   double sky_color[3];
   const DExt* exts;        // book-2 extension records (null when the scene has none)
-  double time0, time1;     // camera shutter (set per render call; moving spheres read it)
+  double time0, time1;     // camera shutter (set per render call)
+  const double* shutter;   // device copy of {time0, time1}: moving spheres read it at the use site (an
+                           // opaque pointer: held in SGPRs across the megakernel's loop the two doubles spill)
 };
 
 struct DCamera {
@@ -212,10 +214,10 @@ struct DWork {
   // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
   // segment, then steal from the next segments that still hold units
   uint32_t seg_len, n_segs;
-  // shared queue (n_segs == 0): units per atomic while more than q_tail units remain after the wave's
-  // previous window, kSegmentWindow after that (plan.h; read through work_const where a unit is taken)
+  // shared queue (n_segs == 0): units [0, q_bulk_end) in q_window-unit windows from unit_counter[0],
+  // [q_bulk_end, n_units) in kSegmentWindow-unit windows from unit_counter[kTailCounter] (plan.h)
   uint32_t q_window, pad_q;
-  uint64_t q_tail;
+  uint64_t q_bulk_end;
 };
 
 // Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot
@@ -226,6 +228,7 @@ struct DCounters {
 };
 constexpr int kCounterSlots = 64;
 // (work units a megakernel wave takes per queue atomic: kSegmentWindow / kQueueWindow, plan.h)
+constexpr int kTailCounter = 8;  // the shared queue's tail counter: unit_counter[8], its own 64-B line
 // instrumented build: DCounters.pad slots of the megakernel's phase clocks (PH_STAMP in trace.hip) and
 // traversal step statistics
 enum : int {
@@ -241,11 +244,22 @@ struct KParams {
   unsigned long long* unit_counter;  // work-queue head (one 64-unit batch per fetch)
   DCounters* counters;
   int32_t split_refill;          // split_kernel: idle traversal lanes before a wave claims rays (>= 1)
-  // device copy of `cam` (megakernel): read with scalar loads where a new sample's camera ray is
-  // formed instead of being held in SGPRs across the whole loop (where it spills to VGPR lanes)
-  uint64_t cam_const;
-  uint64_t work_const;           // device copy of `work`, read the same way where a unit is taken
-  uint64_t scene_const;          // device copy of `scene`, read the same way where the sky is shaded
+  // the megakernel's KBlock of this pass (device memory): its rarely used uniforms are read there with
+  // scalar loads at their use sites instead of being held in SGPRs across the whole loop, where they
+  // spill to VGPR lanes and come back one v_readlane each
+  uint64_t kconst;
+};
+
+// Device copy of a pass's launch parameters for the megakernel (KParams.kconst): the camera (read where
+// a new sample's ray is formed), the scene record (the sky, where a missed ray is shaded), the work
+// descriptor and the output / queue / statistics pointers (where a unit is taken or published).
+struct alignas(16) KBlock {
+  DCamera cam;
+  DScene scene;
+  DWork work;
+  double* partial;
+  unsigned long long* unit_counter;
+  DCounters* counters;
 };
 
 // ---- wavefront engine (wavefront.hip): path state of P slots as structure-of-arrays in HBM ----

@@ -74,7 +74,7 @@ void trace_kernel(KParams P) {
 
   // wave-uniform window of unit indices
   unsigned long long w_next = 0, w_end = 0;
-  bool exhausted = false;
+  bool exhausted = false, tail_mode = false;
   // units are taken from per-block segments of the unit space (stealing from other segments once the
   // block's is empty) when DWork.n_segs != 0, else from one global queue.
   // the block's segment, XCD-major: blocks are dealt round-robin to the 8 XCDs, so block b (on XCD
@@ -191,30 +191,34 @@ void trace_kernel(KParams P) {
         idx = w_next + rank;
         w_next += k;
       } else {
-        unsigned long long nb = W.n_units;
-        if (W.n_segs != 0u) {
+        KBlk* kb = kblock(P.kconst);  // (the queue's pointers and sizes, read with scalar loads here)
+        unsigned long long nb = kb->work.n_units;
+        if (kb->work.n_segs != 0u) {
         // the block's segment (consecutive chunks of neighbouring tiles: coherent lanes, the same
         // subtrees in this XCD's L2), then any segment that still holds units: the 64 lanes read 64
         // candidates' counters at once (device-coherent atomic loads) and the wave takes the first
         // non-empty one.  A failed take means that segment is now empty for good (counters only grow),
         // so the search ends after at most n_segs failures.
-        unsigned* ctr = reinterpret_cast<unsigned*>(P.unit_counter);
+        unsigned* ctr = reinterpret_cast<unsigned*>(kb->unit_counter);
         for (;;) {
           unsigned off = 0;
           if (lane == 0) off = atomicAdd(ctr + seg, kSegmentWindow);
           off = (unsigned)__builtin_amdgcn_readfirstlane((int)off);
-          if (off < W.seg_len && (unsigned long long)seg * W.seg_len + off < W.n_units) {
-            nb = (unsigned long long)seg * W.seg_len + off;
+          const uint32_t seg_len = kb->work.seg_len;
+          const unsigned long long n_units = kb->work.n_units;
+          if (off < seg_len && (unsigned long long)seg * seg_len + off < n_units) {
+            nb = (unsigned long long)seg * seg_len + off;
             break;
           }
           bool found = false;
-          for (uint32_t base = 0; base < W.n_segs; base += kWave) {
+          const uint32_t n_segs = kb->work.n_segs;
+          for (uint32_t base = 0; base < n_segs; base += kWave) {
             uint32_t cand = seg + 1u + base + (uint32_t)lane;
-            if (cand >= W.n_segs) cand -= W.n_segs;
+            if (cand >= n_segs) cand -= n_segs;
             bool has = false;
-            if (base + (uint32_t)lane < W.n_segs) {
+            if (base + (uint32_t)lane < n_segs) {
               const unsigned o = __hip_atomic_load(ctr + cand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              has = o < W.seg_len && (unsigned long long)cand * W.seg_len + o < W.n_units;
+              has = o < seg_len && (unsigned long long)cand * seg_len + o < n_units;
             }
             const unsigned long long m = __ballot(has);
             if (m != 0ull) {
@@ -226,27 +230,26 @@ void trace_kernel(KParams P) {
           if (!found) break;
         }
         } else {  // one shared queue (short units: DWork.n_segs = 0)
-          // big windows while more than q_tail units remain, 64-unit windows for the pool's end (plan.h);
-          // the policy is read with scalar loads here, like the unit fetch.  The wave's own view of the
-          // counter (its previous window's end) is stale by the units every other wave took since — most
-          // for the slowest waves, whose big windows would make the frame's tail — so near the end the
-          // counter's current value decides (one atomic load per take).
-          KWork* kw = (KWork*)(uintptr_t)P.work_const;
-          asm volatile("" : "+s"(kw));
-          const unsigned long long tail = kw->q_tail;
-          unsigned long long left = W.n_units > w_end ? W.n_units - w_end : 0ull;
-          if (left <= 4ull * tail) {
-            unsigned long long cur = 0;
-            if (lane == 0) cur = __hip_atomic_load(P.unit_counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            cur = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(cur >> 32)) << 32) |
-                  (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)cur);
-            left = W.n_units > cur ? W.n_units - cur : 0ull;
+          // the pool's bulk [0, q_bulk_end) in q_window-unit windows (few atomics on the one counter), its
+          // last units [q_bulk_end, n_units) from a second counter in 64-unit windows, so that no wave
+          // starts a long window at the pool's end (plan.h).  q_bulk_end is a multiple of q_window: a bulk
+          // window never straddles into the tail.  A wave whose bulk take comes back empty stays on the tail.
+          const unsigned long long bulk_end = kb->work.q_bulk_end;
+          nb = bulk_end;
+          if (!tail_mode) {
+            win = kb->work.q_window;
+            if (lane == 0) nb = atomicAdd(kb->unit_counter, (unsigned long long)win);
+            nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
+                 (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
+            tail_mode = nb >= bulk_end;
           }
-          win = left > tail ? kw->q_window : kSegmentWindow;
-          nb = 0;
-          if (lane == 0) nb = atomicAdd(P.unit_counter, (unsigned long long)win);
-          nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
-               (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
+          if (tail_mode) {
+            win = kSegmentWindow;
+            unsigned long long off = 0;
+            if (lane == 0) off = atomicAdd(kb->unit_counter + kTailCounter, (unsigned long long)win);
+            nb = bulk_end + (((unsigned long long)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
+                             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)off));
+          }
         }
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
@@ -254,12 +257,12 @@ void trace_kernel(KParams P) {
         if (nb >= W.n_units) exhausted = true;
       }
       if (need && idx < W.n_units) {
+        KBlk* kb = kblock(P.kconst);
         // unit -> (local tile, chunk, lane-in-tile); tile-major so a window = 64 neighbours.  32-bit
         // quotients (the host keeps n_units < 2^32): far cheaper than 64-bit ones.  The work
         // descriptor and the image size are read here with scalar loads, like the camera below.
-        KWork* kw = (KWork*)(uintptr_t)P.work_const;
-        KCamera* kc = (KCamera*)(uintptr_t)P.cam_const;
-        asm volatile("" : "+s"(kw), "+s"(kc));
+        KWork* kw = &kb->work;
+        KCamera* kc = &kb->cam;
         const uint32_t pt = (uint32_t)kw->n_chunks * (uint32_t)kTilePixels, i32 = (uint32_t)idx;
         const uint32_t lt = udiv(i32, UDiv{kw->div_unit_tile.m, kw->div_unit_tile.s1, kw->div_unit_tile.s2});  // i32 / pt
         const uint32_t g32 = lt * (uint32_t)kw->tile_world + (uint32_t)kw->tile_rank;
@@ -313,9 +316,7 @@ void trace_kernel(KParams P) {
       PH_COUNT(11);
       // the camera read with scalar loads here (an opaque copy of its address keeps them from being
       // hoisted): held in SGPRs across the loop it spills to VGPR lanes, ~66 v_readlane per iteration
-      KCamera* kc = (KCamera*)(uintptr_t)P.cam_const;
-      asm volatile("" : "+s"(kc));
-      camera_ray_drawn(*kc, jx, jy, rs, o, d);
+      camera_ray_drawn(kblock(P.kconst)->cam, jx, jy, rs, o, d);
     }
     PH_STAMP(kPhCamera);
     if (active) {
@@ -329,9 +330,7 @@ void trace_kernel(KParams P) {
 #if RT_KSCENE
         // the sky's kind and colour read with scalar loads here, like the camera (held in SGPRs across
         // the loop they spill to VGPR lanes)
-        KScene* ks = (KScene*)(uintptr_t)P.scene_const;
-        asm volatile("" : "+s"(ks));
-        emit = sky_unit(*ks, un);
+        emit = sky_unit(kblock(P.kconst)->scene, un);
 #else
         emit = sky_unit(S, un);
 #endif
@@ -351,7 +350,7 @@ void trace_kernel(KParams P) {
     // a finished unit publishes its in-order sample sum (render.rs:58-69: *buf_c = c)
     if (publish) {
       PH_COUNT(24);
-      double* dst = P.partial + (size_t)pub_index * 3;
+      double* dst = kblock(P.kconst)->partial + (size_t)pub_index * 3;
       dst[0] = sum.x;
       dst[1] = sum.y;
       dst[2] = sum.z;
@@ -360,7 +359,7 @@ void trace_kernel(KParams P) {
     if (regen) {
       att = V(1.0, 1.0, 1.0);
       em = V(0.0, 0.0, 0.0);
-      depth_left = W.max_depth;  // >= 1: max_depth == 0 frames are written by render_window itself
+      depth_left = kblock(P.kconst)->work.max_depth;  // >= 1: max_depth == 0 frames are written by render_window itself
       active = true;
     }
     PH_STAMP(kPhTail);
@@ -383,7 +382,7 @@ void trace_kernel(KParams P) {
     }
 #endif
     if (visits > (1u << 30) || ptests > (1u << 30)) {  // (never within a frame of today's sizes)
-      DCounters* cs = P.counters + (blockIdx.x % kCounterSlots);
+      DCounters* cs = kblock(P.kconst)->counters + (blockIdx.x % kCounterSlots);
       atomicAdd(&cs->node_visits, (unsigned long long)visits);
       atomicAdd(&cs->prim_tests, (unsigned long long)ptests);
       visits = ptests = 0;
@@ -400,10 +399,10 @@ void trace_kernel(KParams P) {
   }
 #ifdef RT_PHASE_TIMING
   for (int off = 32; off > 0; off >>= 1) ph_lane_steps += __shfl_down(ph_lane_steps, off);
-  if (lane == 0) atomicAdd(&P.counters[blockIdx.x % kCounterSlots].pad[kPhLaneSteps], ph_lane_steps);
+  if (lane == 0) atomicAdd(&kblock(P.kconst)->counters[blockIdx.x % kCounterSlots].pad[kPhLaneSteps], ph_lane_steps);
 #endif
   if (lane == 0) {
-    DCounters* cs = P.counters + (blockIdx.x % kCounterSlots);
+    DCounters* cs = kblock(P.kconst)->counters + (blockIdx.x % kCounterSlots);
     atomicAdd(&cs->segments, n_seg);
     atomicAdd(&cs->samples, n_samp);
     atomicAdd(&cs->node_visits, n_vis);

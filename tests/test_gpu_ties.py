@@ -102,7 +102,8 @@ def test_rect_coplanar_with_rectbox_face_tie(gpu):
         rng = np.random.default_rng(12)
         tgt = np.column_stack([rng.uniform(-0.9, 0.9, 256), np.zeros(256), rng.uniform(-3.9, -2.1, 256)])
         org = tgt + np.column_stack([rng.uniform(-1, 1, 256), rng.uniform(0.5, 3, 256), rng.uniform(-1, 1, 256)])
-        org[:32, 0], org[:32, 2] = tgt[:32, 0], tgt[:32, 2]  # 32 vertical rays (1/d exact: the reference's rect wins)
+        # 32 vertical rays of direction (0, -1, 0): 1/d is exact, so the box's slab entry at y = 0 IS the tie
+        org[:32] = tgt[:32] + np.array([0.0, 1.0, 0.0])
         rays = np.hstack([org, tgt - org])
         dev = gpu.hit(rays, 0.001, float("inf"), traversal="render")
         n_ref_rect = 0

@@ -115,8 +115,10 @@ def tree_hit(spheres, ray, t_min=0.0, t_max=MAX):
 
 
 def test_tree_size_of_tree_node():
-    # bbox_tree.rs:102-107 pins the Rust TreeNode at 72 B (bbox 48 + enum).  The device layout is a
-    # BVH2 node with both child boxes inline: 112 B for two boxes = 56 B per box (< 72 B).
+    # bbox_tree.rs:102-107 pins the Rust TreeNode at 72 B (bbox 48 + enum).  Its C-ABI counterpart, the
+    # inspection record rt_bvh_node (rt_bvh_build_host), is 64 B: box 48 + leaf / lhs / rhs / pad 4 x 4 B
+    # (the enum's tag folded into leaf = -1).  The device's own layouts are rt_layout.h's (DNode 112 B,
+    # DNode4F 160 B, DNode4C 112 B; checked there by static_assert).
     import raytracer._native as N
     assert C.sizeof(N.rt_bvh_node) == 64
 

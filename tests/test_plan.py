@@ -26,7 +26,7 @@ def plan(tmp_path_factory):
         args = [str(x) for call in calls for x in call]
         out = subprocess.run([exe] + args, check=True, capture_output=True, text=True, timeout=60).stdout.split("\n")
         keys = ("chunk", "n_chunks", "per_pass", "passes", "partial_bytes", "segments", "ok", "queue_window",
-                "queue_tail")
+                "queue_tail", "bulk_end")
         res = [dict(zip(keys, map(int, line.split()))) for line in out if line.strip()]
         return res if len(res) > 1 else res[0]
     return run
@@ -40,8 +40,9 @@ def test_headline_frame_one_pass(plan):
     # random_scene 1200x800 @ 500 spp: 8-sample units, one pass of 1.45 GB, per-block segments
     n = pixels(1200, 800)
     p = plan((n, 500, MEGA, LANES, 0, DEFAULT))
+    tail = LANES // 64 * 256
     assert p == dict(chunk=8, n_chunks=63, per_pass=63, passes=1, partial_bytes=n * 63 * 24, segments=1, ok=1,
-                     queue_window=256, queue_tail=LANES // 64 * 256)
+                     queue_window=256, queue_tail=tail, bulk_end=(n * 63 - tail) // 256 * 256)
     assert p["partial_bytes"] == 1_451_520_000
 
 
@@ -140,19 +141,26 @@ def test_every_pass_fits_its_bound(plan):
 
 def test_shared_queue_windows_shrink_for_the_pool_end(plan):
     # one-sample units on the shared queue (cfg1 400x225 @ 50: 17 units per lane; the 8-rank share of the
-    # headline: 229): 256-unit windows (4 units per lane, one queue atomic per 256 units — the 8-rank frame
-    # 24.1 -> 22.9 ms) while more than one round of them remains (256 units per resident wave, 1 M units on
-    # MI355X), 64-unit windows for the rest — so no wave starts a 4-unit-per-lane window at the pool's end
-    # (cfg1: 256-unit windows to the end ran 1490 Msamples/s, 64-unit windows 1830; gpurun_out/r05a, r05b)
+    # headline: 229): the pool's bulk in 256-unit windows (4 units per lane, one atomic per 256 units on the
+    # one counter — the 8-rank frame 24.1 -> 22.9 ms), its last round of them (256 units per resident wave,
+    # 1 M units on MI355X) from a second counter in 64-unit windows, so no wave starts a 4-unit-per-lane
+    # window at the pool's end (cfg1: 256-unit windows to the end ran 1490 Msamples/s, 64-unit windows 1830;
+    # gpurun_out/r05a, r05b)
     cfg1 = plan((pixels(400, 225), 50, MEGA, LANES, 0, DEFAULT))
     r8 = plan((pixels(1200, 800) // 8, 500, MEGA, LANES, 0, DEFAULT))
-    for p in (cfg1, r8):
+    tail = (LANES // 64) * 256
+    for p, n in ((cfg1, pixels(400, 225)), (r8, pixels(1200, 800) // 8)):
         assert p["segments"] == 0 and p["chunk"] == 1
-        assert p["queue_window"] == 256 and p["queue_tail"] == (LANES // 64) * 256
-    units = lambda p, n: n * p["n_chunks"]
-    # cfg1: 4.6 M units, so the last 1 M (22 %) go in 64-unit windows; the 8-rank share: 1.7 % of 60 M
-    assert 0.2 < cfg1["queue_tail"] / units(cfg1, pixels(400, 225)) < 0.25
-    assert r8["queue_tail"] / units(r8, pixels(1200, 800) // 8) < 0.02
-    # the tail scales with the resident waves (a smaller device or a narrower launch)
+        assert p["queue_window"] == 256 and p["queue_tail"] == tail
+        units = n * p["per_pass"]
+        # the bulk ends on a window boundary (a bulk window never straddles into the tail) and leaves the
+        # tail, plus less than one window, to the second counter
+        assert p["bulk_end"] % 256 == 0 and tail <= units - p["bulk_end"] < tail + 256
+    # cfg1: 4.6 M units, the last 1 M (22 %) in 64-unit windows; the 8-rank share: 1.7 % of 60 M
+    assert 0.2 < (pixels(400, 225) * 50 - cfg1["bulk_end"]) / (pixels(400, 225) * 50) < 0.25
+    assert (pixels(1200, 800) // 8 * 500 - r8["bulk_end"]) / (pixels(1200, 800) // 8 * 500) < 0.02
+    # the tail scales with the resident waves; a pool no larger than the tail is all tail
     small = plan((pixels(400, 225), 50, MEGA, 32 * 1024, 0, DEFAULT))
     assert small["queue_tail"] == 512 * 256
+    tiny = plan((pixels(64, 64), 4, MEGA, LANES, 1, DEFAULT))
+    assert tiny["bulk_end"] == 0

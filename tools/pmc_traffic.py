@@ -49,7 +49,8 @@ def main(src, dst, workload, bvh):
            "hbm_bytes_per_launch": bytes_per_launch,
            "rocprof_avg_ns": float(trace["AverageNs"]), "rocprof_calls": int(trace["Calls"])}
     json.dump(out, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
-    json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip("/")), "traffic.json"), "w"), indent=1)
+    if not os.environ.get("PMC_NO_TOP"):  # (a config other than the headline: keep profiles/traffic.json)
+        json.dump(out, open(os.path.join(os.path.dirname(dst.rstrip("/")), "traffic.json"), "w"), indent=1)
     print(json.dumps(out))
 
 

@@ -10,6 +10,7 @@ of that frame (one per sample pass) are summed, and every pass sees the same det
   f64 FLOPs   = (ADD_F64 + MUL_F64 + 2 FMA_F64) wave-instructions x 64 x lane_util
 
 usage: python tools/pmc_valu.py <profiles/TAG> <waves_per_simd> <pass_dir> [<pass_dir> ...]
+(PMC_NO_TOP=1: write <profiles/TAG>/valu.json only, not the top-level copy bench.py reads)
 """
 import csv
 import glob
@@ -70,7 +71,8 @@ def main(dst, waves_per_simd, *passes):
         "source": f"{dst}: " + ", ".join(sources),
     }
     json.dump(v, open(os.path.join(dst, "valu.json"), "w"), indent=1)
-    json.dump(v, open(os.path.join(os.path.dirname(dst.rstrip("/")), "valu.json"), "w"), indent=1)
+    if not os.environ.get("PMC_NO_TOP"):  # (a config other than the headline: keep profiles/valu.json)
+        json.dump(v, open(os.path.join(os.path.dirname(dst.rstrip("/")), "valu.json"), "w"), indent=1)
     print(json.dumps({k: v[k] for k in v if k != "counters"}))
 
 
