@@ -303,20 +303,26 @@ def compare_frames(ref, got, exact, rel=1e-12):
                     f"{n} of {ref.size} channels beyond {rel:g} relative, max |d| {worst:.3g}")
 
 
-def sharded_frame(args, dev, comm, rank, world, torch, rt, cam, settings, part):
+def sharded_frame(args, dev, comm, rank, world, torch, rt, cam, settings, part, ran=None):
     """One multi-rank frame through the job's exchange: rt_render_sharded (RCCL) or, in a gloo rehearsal,
     the same exchange by torch.distributed (raytracer/parallel.py).  Rank 0 gets the [H][W][3] sums
-    (a CUDA tensor), the other ranks None."""
+    (a CUDA tensor), the other ranks None.  `ran` (a list) records whether this rank launched a render:
+    a gloo rank whose sample share is empty (more ranks than samples) launches none, so it has no
+    counters (rt_render_sharded runs an empty-range render instead)."""
     from raytracer.parallel import gather_tiles, reduce_sample_bands, sample_share
     W, H = cam.image_width, cam.image_height
     sh = torch.cuda.current_stream().cuda_stream
     out = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda") if rank == 0 else None
+    if ran is not None:
+        ran[:] = [True]
     if comm is not None:
         dev.render_sharded(comm, cam, settings, out.data_ptr() if rank == 0 else 0, sh)
         return out
     if part == "samples":
         b, e = sample_share(0, settings.samples, rank, world)
         local = torch.zeros((H, W, 3), dtype=torch.float64, device="cuda")
+        if ran is not None:
+            ran[:] = [e > b]
         if e > b:
             s = rt.RenderSettings(**{**settings.__dict__, "sample_begin": b, "sample_count": e - b, "tile_rank": 0,
                                      "tile_world": 1})
@@ -446,6 +452,8 @@ def main():
     ev_dev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
     device_ms = []
 
+    ran = [True]  # this rank launched a render in the step (a gloo rank with an empty sample share: none)
+
     def step():
         ev_dev[0].record(stream)
         if world == 1:
@@ -454,7 +462,7 @@ def main():
             dev.render_sharded(comm, cam, settings, accum.data_ptr() if rank == 0 else 0, sh)
         else:  # gloo rehearsal (ranks sharing one GPU cannot form an RCCL communicator): the same exchange
             out = sharded_frame(args, dev, None, rank, world, torch, rt, cam,
-                                rt.RenderSettings(**{**settings.__dict__, "partition": partition}), partition)
+                                rt.RenderSettings(**{**settings.__dict__, "partition": partition}), partition, ran)
             if rank == 0:
                 accum.copy_(out)
         ev_dev[1].record(stream)
@@ -471,9 +479,11 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-        c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
         ev_dev[1].synchronize()
         device_ms.append(ev_dev[0].elapsed_time(ev_dev[1]))
+        if not ran[0]:
+            continue
+        c = dev.counters()  # waits for this step's trace + reduce events (no extra work on the GPU)
         kernel_ms.append(c.kernel_ms)
         segments.append(c.segments)
         samples.append(c.samples)
@@ -492,12 +502,17 @@ def main():
     total_samples = W * H * args.spp * args.steps
     value = total_samples / elapsed / 1e6
     # per trace-kernel launch (a frame whose partial sums exceed the scratch bound runs in several sample
-    # passes, one launch each): algorithmic bytes of a launch / its average duration
+    # passes, one launch each): algorithmic bytes of a launch / its average duration.  Rank 0 may have traced
+    # nothing (a sample partition with more ranks than samples per pixel): then the kernel figures are null.
+    if not laps:
+        laps = [(0,) * 12]
+        kernel_ms, segments, samples = [0.0], [0], [0]
     launches = max(1, laps[-1][8])
     k_ms = float(np.mean(kernel_ms)) / launches
     seg = float(np.mean(segments)) / launches
-    achieved = BYTES_PER_SEGMENT * seg / (k_ms * 1e-3) / 1e9
-    achieved_f64 = BYTES_PER_SEGMENT_F64 * seg / (k_ms * 1e-3) / 1e9
+    traced = k_ms > 0.0 and seg > 0.0
+    achieved = BYTES_PER_SEGMENT * seg / (k_ms * 1e-3) / 1e9 if traced else None
+    achieved_f64 = BYTES_PER_SEGMENT_F64 * seg / (k_ms * 1e-3) / 1e9 if traced else None
     traffic = None
     tfile = os.path.join(REPO, "profiles", "traffic.json")
     if world == 1 and os.path.exists(tfile):  # (measured per N=1 launch; a rank's launch is smaller)
@@ -533,14 +548,16 @@ def main():
                    # counted by the instrumented build only (RT_PHASE_TIMING): null here
                    "node_tests_per_segment": round(laps[-1][6] / max(segments[-1], 1), 3) if laps[-1][6] else None,
                    "prim_tests_per_segment": round(laps[-1][7] / max(segments[-1], 1), 3) if laps[-1][7] else None},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2) if traced else None, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if traced else None,
+                     "traffic": traffic,
                      "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3), "launches_per_step": launches,
                      "bytes_per_segment": BYTES_PER_SEGMENT, "segments_per_launch": int(seg),
-                     "f64_state": {"bytes_per_segment": BYTES_PER_SEGMENT_F64, "achieved": round(achieved_f64, 2),
-                                   "frac": round(achieved_f64 / HBM_PEAK_GBS, 5)},
-                     "measured_hbm_gbs": round(traffic / (k_ms * 1e-3) / 1e9, 2) if traffic else None,
-                     "valu": valu_block(seg, k_ms, W, H, args) if world == 1 else None},
+                     "f64_state": {"bytes_per_segment": BYTES_PER_SEGMENT_F64,
+                                   "achieved": round(achieved_f64, 2) if traced else None,
+                                   "frac": round(achieved_f64 / HBM_PEAK_GBS, 5) if traced else None},
+                     "measured_hbm_gbs": round(traffic / (k_ms * 1e-3) / 1e9, 2) if traffic and traced else None,
+                     "valu": valu_block(seg, k_ms, W, H, args) if world == 1 and traced else None},
         "cpu_baseline": None,
     }
     mrc = None

@@ -1,8 +1,7 @@
 // plan_check — prints rt::plan_samples (csrc/rt/plan.h: unit length, sample passes, scratch) for the
 // calls given on the command line, so tests/test_plan.py checks the planning rules on the CPU.
 //   plan_check <n_pix> <count> <engine> <lanes> <sample_chunk> <budget_bytes> [...6 more per call]
-// prints one line per call: chunk n_chunks per_pass passes partial_bytes segments ok queue_window queue_tail
-// bulk_end (of a full pass: n_pix * per_pass units)
+// prints one line per call: chunk n_chunks per_pass passes partial_bytes segments ok queue_window
 #include <cstdio>
 #include <cstdlib>
 
@@ -16,10 +15,8 @@ int main(int argc, char** argv) {
   for (int i = 1; i + 5 < argc; i += 6) {
     const rt::SamplePlan P = rt::plan_samples(std::atoll(argv[i]), std::atoi(argv[i + 1]), std::atoi(argv[i + 2]),
                                               std::atoll(argv[i + 3]), std::atoi(argv[i + 4]), std::atoll(argv[i + 5]));
-    const unsigned long long units = (unsigned long long)std::atoll(argv[i]) * (unsigned long long)P.per_pass;
-    std::printf("%d %d %d %d %lld %d %d %u %llu %llu\n", P.chunk, P.n_chunks, P.per_pass, P.passes, P.partial_bytes,
-                P.segments ? 1 : 0, P.ok ? 1 : 0, P.queue_window, P.queue_tail,
-                rt::bulk_end(units, P.queue_tail, P.queue_window));
+    std::printf("%d %d %d %d %lld %d %d %u\n", P.chunk, P.n_chunks, P.per_pass, P.passes, P.partial_bytes,
+                P.segments ? 1 : 0, P.ok ? 1 : 0, P.queue_window);
   }
   return 0;
 }
