@@ -640,11 +640,32 @@ static void* dupmem(const void* p, size_t n) {
   return q;
 }
 
+/* Book-2 (extension): Translate(RotateY(sphere)) of a plain sphere is the sphere about the moved
+ * centre, so such an instance is flattened into a world-space sphere before anything else reads it —
+ * centre (cs cx + sn cz + off.x, cy + off.y, -sn cx + cs cz + off.z), the same formula that maps an
+ * instance's hit point back to the world (ext_object_hit) — and takes the reference sphere path.  The
+ * host (rt_api.cpp flat_object) flattens identically.  Exact in real arithmetic; the records differ
+ * from per-ray instancing at the last bit. */
+static void flatten_instanced_sphere(rt_object* o) {
+  if (o->geometry != RT_GEOM_SPHERE || !o->transform || o->medium) return;
+  double cs, sn;
+  rotate_y_cs(o, &cs, &sn);
+  const double cx = o->p[0], cy = o->p[1], cz = o->p[2];
+  o->p[0] = (cs * cx + sn * cz) + o->offset[0];
+  o->p[1] = cy + o->offset[1];
+  o->p[2] = (-sn * cx + cs * cz) + o->offset[2];
+  o->transform = 0;
+  o->rotate_y_deg = 0.0;
+  o->offset[0] = o->offset[1] = o->offset[2] = 0.0;
+}
+
 or_scene* or_scene_new(const rt_scene_desc* d) {
   if (!d || d->n_objects < 0) return NULL;
   or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
   s->desc = *d;
   s->objects = (rt_object*)dupmem(d->objects, sizeof(rt_object) * (size_t)d->n_objects);
+  for (int32_t i = 0; i < d->n_objects; ++i) flatten_instanced_sphere(&s->objects[i]);
+  s->desc.objects = s->objects;
   s->materials = (rt_material*)dupmem(d->materials, sizeof(rt_material) * (size_t)d->n_materials);
   s->textures = (rt_texture*)dupmem(d->textures, sizeof(rt_texture) * (size_t)d->n_textures);
   s->perlin = (rt_perlin_table*)dupmem(d->perlin, sizeof(rt_perlin_table) * (size_t)d->n_perlin);
@@ -662,7 +683,7 @@ or_scene* or_scene_new(const rt_scene_desc* d) {
   if (n > 0) {
     /* constructor.rs:9-36 construct_tree: every geometry is bounded, so all objects are leaves */
     aabb_t* boxes = (aabb_t*)malloc(sizeof(aabb_t) * (size_t)n);
-    for (int32_t i = 0; i < n; ++i) object_bbox(&d->objects[i], &boxes[i]);
+    for (int32_t i = 0; i < n; ++i) object_bbox(&s->objects[i], &boxes[i]);
     build_t b;
     b.leaf_box = boxes;
     b.n = n;

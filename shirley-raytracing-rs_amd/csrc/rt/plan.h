@@ -23,8 +23,7 @@ constexpr int kWfDefaultChunk = 8;          // wavefront engine's unit length (i
 constexpr long long kDefaultScratchMiB = 8192;
 
 // Work units a megakernel wave takes per queue atomic (multiples of the wave size): kSegmentWindow from a
-// block's own segment, and from the one shared queue kQueueWindow while many units remain, then
-// kSegmentWindow for the pool's last units (SamplePlan.queue_tail).
+// block's own segment; from the one shared queue kQueueWindow or kSegmentWindow (SamplePlan.queue_window).
 constexpr unsigned kSegmentWindow = 64;
 constexpr unsigned kQueueWindow = 256;
 
@@ -35,10 +34,7 @@ struct SamplePlan {
   int passes = 0;
   long long partial_bytes = 0;  // scratch of one pass
   bool segments = false;  // megakernel per-block unit segments (units of >= 4 samples)
-  // shared queue (segments off): the pool's units but its last queue_tail go in queue_window-unit
-  // windows, those in kSegmentWindow-unit windows (bulk_end)
-  unsigned queue_window = kQueueWindow;
-  unsigned long long queue_tail = 0;
+  unsigned queue_window = kQueueWindow;  // shared queue (segments off): units per queue atomic
   bool ok = true;        // false: a pass cannot index one chunk of the frame in 32 bits
 };
 
@@ -80,12 +76,18 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   // 24.5 -> 23.4 ms with 256-unit windows (512: 23.8, 1024: 25.2; with segments 128 / 256 cost the
   // headline 0.4 / 1.8 %), profiles/r04/shard_scan/.
   P.segments = engine == RT_ENGINE_MEGAKERNEL && chunk >= 4;
-  // The shared queue's windows shrink for the pool's end: a wave's last window decides when it finishes,
-  // and 256 units are 4 per lane — on a small frame (cfg1 400x225 @ 50: 17 units per lane) a ragged end
-  // of up to 4 units per lane.  So the pool's last round of 256-unit windows (256 units per resident
-  // wave) is served in 64-unit windows from a second counter (bulk_end below; trace.hip).
-  P.queue_window = kQueueWindow;
-  P.queue_tail = (unsigned long long)std::max(1LL, lanes / 64) * kQueueWindow;
+  // The shared queue's window: 256 units (4 per lane) per atomic where a lane has >= 128 units (the
+  // 8-rank share of the headline, 229: one counter for all waves, 24.1 -> 22.9 ms against 64-unit
+  // windows), else 64.  A wave's time is the sum of its windows', whose cost follows the tile they
+  // came from (sky vs glass ground): with few units per lane, 4-per-lane windows leave each wave only
+  // a few tiles to average over, and the waves end far apart — cfg1 400x225 @ 50 (17.7 units per lane)
+  // ran 1490 Msamples/s with 256-unit windows and 1830-1880 with 64 (gpurun_out/r05a, r05f1); serving
+  // just the pool's last 1 M units in 64-unit windows from a second counter did not help (r05f1: the
+  // imbalance builds up over the whole frame, not at its end), nor did shrinking windows near the end.
+  {
+    const long long units = n_pix * (long long)P.n_chunks;
+    P.queue_window = (lanes > 0 && units >= 128 * lanes) ? kQueueWindow : kSegmentWindow;
+  }
 
   // sample passes: at most `budget` bytes of [chunks][pixels][3] f64 partial sums per pass
   const long long chunk_bytes = std::max<long long>(1, n_pix * 3 * (long long)sizeof(double));
@@ -103,14 +105,6 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   P.per_pass = (P.n_chunks + P.passes - 1) / P.passes;  // even passes
   P.partial_bytes = std::max<long long>(1, n_pix * P.per_pass * 3) * (long long)sizeof(double);
   return P;
-}
-
-// The shared queue's bulk: units [0, bulk_end) go in `window`-unit windows, the rest in 64-unit windows.
-// A multiple of the window (a bulk window never straddles into the tail), and 0 when the pool holds no
-// more than the tail.
-inline unsigned long long bulk_end(unsigned long long n_units, unsigned long long tail, unsigned window) {
-  const unsigned long long w = std::max(1u, window);
-  return n_units > tail ? (n_units - tail) / w * w : 0ull;
 }
 
 }  // namespace rt

@@ -183,6 +183,32 @@ void rotate_y_cs(const rt_object& o, double& cs, double& sn) {
   cs = std::cos(rad);
   sn = std::sin(rad);
 }
+// Book-2: Translate(RotateY(sphere)) of a plain sphere is the sphere about the moved centre — flattened
+// into a world-space sphere before the tree is built, by the formula that maps an instance's hit point
+// back to the world, so the instances take the reference sphere path (sphere leaf loop, no per-leaf ray
+// transform).  The oracle flattens identically (oracle.c flatten_instanced_sphere).  DESIGN.md §10.
+rt_object flat_object(const rt_object& o) {
+  rt_object f = o;
+  if (o.geometry != RT_GEOM_SPHERE || !o.transform || o.medium) return f;
+  double cs, sn;
+  rotate_y_cs(o, cs, sn);
+  const double cx = o.p[0], cy = o.p[1], cz = o.p[2];
+  f.p[0] = (cs * cx + sn * cz) + o.offset[0];
+  f.p[1] = cy + o.offset[1];
+  f.p[2] = (-sn * cx + cs * cz) + o.offset[2];
+  f.transform = 0;
+  f.rotate_y_deg = 0.0;
+  f.offset[0] = f.offset[1] = f.offset[2] = 0.0;
+  return f;
+}
+// A scene description whose objects are flat_object's (the objects live in `store`).
+rt_scene_desc flat_scene(const rt_scene_desc* d, std::vector<rt_object>& store) {
+  store.resize((size_t)std::max(0, d->n_objects));
+  for (int i = 0; i < d->n_objects; ++i) store[i] = flat_object(d->objects[i]);
+  rt_scene_desc f = *d;
+  f.objects = store.data();
+  return f;
+}
 // moving_sphere.h center(time), the device's formula (the bounding box uses it at time0 and time1)
 void moving_center(const rt_object& o, double tm, double* c) {
   const double s = (tm - o.q[3]) / (o.q[4] - o.q[3]);
@@ -944,7 +970,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
   c->host_blocks.assign(passes, KBlock{});
   const uint64_t nseg = (uint64_t)std::max(1, c->cu_count * std::max(1, c->blocks_per_cu));
   {
-    const size_t bytes = std::max<size_t>(128, (size_t)nseg * sizeof(uint32_t));  // (>= the tail counter's line)
+    const size_t bytes = std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t));
     st = ensure(c, c->unit_counter, bytes);
     if (st) return st;
     kp.unit_counter = static_cast<unsigned long long*>(c->unit_counter.p);
@@ -1000,12 +1026,8 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     w.n_segs = plan.segments ? (uint32_t)nseg : 0u;
     w.seg_len = (uint32_t)std::max<uint64_t>(kSegmentWindow, (per + kSegmentWindow - 1) / kSegmentWindow * kSegmentWindow);
     w.q_window = plan.queue_window;
-    uint64_t tail = plan.queue_tail;
-    if (const char* e = getenv("SHIRLEY_WINDOW"))  // (tuning: the shared queue's bulk window, units)
+    if (const char* e = getenv("SHIRLEY_WINDOW"))  // (tuning: the shared queue's window, units)
       w.q_window = (uint32_t)std::max(1, atoi(e) / kWave) * (uint32_t)kWave;
-    if (const char* e = getenv("SHIRLEY_QUEUE_TAIL"))  // (tuning: units of the tail served in 64-unit windows)
-      tail = (uint64_t)std::max(0LL, atoll(e));
-    w.q_bulk_end = bulk_end(w.n_units, tail, w.q_window);
     // the device copy is taken after every field is set (the kernel may read any of them)
     KBlock& kb = c->host_blocks[k];
     kb.cam = kp.cam;
@@ -1017,7 +1039,7 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
     void* kdev = static_cast<KBlock*>(c->kcam.p) + k;
     HIP_TRY(c, hipMemcpyAsync(kdev, &kb, sizeof(KBlock), hipMemcpyHostToDevice, s));
     kp.kconst = (uint64_t)(uintptr_t)kdev;
-    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(128, (size_t)nseg * sizeof(uint32_t)), s));
+    HIP_TRY(c, hipMemsetAsync(c->unit_counter.p, 0, std::max<size_t>(64, (size_t)nseg * sizeof(uint32_t)), s));
     HIP_TRY(c, hipEventRecord(c->pass_ev[2 * k], s));
     if (engine == RT_ENGINE_WAVEFRONT) {
       st = run_wavefront(c, kp, timing, s);
@@ -1115,6 +1137,10 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   c->have_scene = false;
+  const uint64_t digest = scene_digest(d, builder);  // (of the description as given)
+  std::vector<rt_object> flat;
+  const rt_scene_desc fd = flat_scene(d, flat);
+  d = &fd;
 
   BuiltTree tree = build_tree(d, builder);
   std::vector<DNode> nodes;
@@ -1372,7 +1398,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->stats.device_bytes = (int64_t)(nodes.size() * sizeof(DNode) + prims.size() * sizeof(DPrim) +
                                     mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex) +
                                     perl.size() * sizeof(DPerlin) + texels.size());
-  c->digest = scene_digest(d, builder);
+  c->digest = digest;
   c->have_scene = true;
   return RT_OK;
 }
@@ -1600,7 +1626,9 @@ int rt_counters_get(rt_ctx* c, rt_counters* out) {
 int rt_bvh_build_host(const rt_scene_desc* d, int32_t builder, int32_t* n_nodes, rt_bvh_node* nodes, int32_t* root) {
   if (!d || !n_nodes) return RT_E_INVALID;
   if (validate(nullptr, d)) return RT_E_INVALID;
-  BuiltTree t = build_tree(d, builder);
+  std::vector<rt_object> flat;
+  const rt_scene_desc fd = flat_scene(d, flat);
+  BuiltTree t = build_tree(&fd, builder);
   if (nodes) {
     if (*n_nodes < (int32_t)t.nodes.size()) return RT_E_INVALID;
     for (size_t i = 0; i < t.nodes.size(); ++i) {

@@ -214,10 +214,8 @@ struct DWork {
   // segments), each with its own counter in unit_counter[]; a block's waves take windows from their
   // segment, then steal from the next segments that still hold units
   uint32_t seg_len, n_segs;
-  // shared queue (n_segs == 0): units [0, q_bulk_end) in q_window-unit windows from unit_counter[0],
-  // [q_bulk_end, n_units) in kSegmentWindow-unit windows from unit_counter[kTailCounter] (plan.h)
+  // shared queue (n_segs == 0): units a wave takes per atomic (plan.h)
   uint32_t q_window, pad_q;
-  uint64_t q_bulk_end;
 };
 
 // Statistics counters, kCounterSlots copies one 128-B line apart: a block adds into slot
@@ -228,7 +226,6 @@ struct DCounters {
 };
 constexpr int kCounterSlots = 64;
 // (work units a megakernel wave takes per queue atomic: kSegmentWindow / kQueueWindow, plan.h)
-constexpr int kTailCounter = 8;  // the shared queue's tail counter: unit_counter[8], its own 64-B line
 // instrumented build: DCounters.pad slots of the megakernel's phase clocks (PH_STAMP in trace.hip) and
 // traversal step statistics
 enum : int {

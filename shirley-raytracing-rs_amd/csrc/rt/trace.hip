@@ -74,7 +74,7 @@ void trace_kernel(KParams P) {
 
   // wave-uniform window of unit indices
   unsigned long long w_next = 0, w_end = 0;
-  bool exhausted = false, tail_mode = false;
+  bool exhausted = false;
   // units are taken from per-block segments of the unit space (stealing from other segments once the
   // block's is empty) when DWork.n_segs != 0, else from one global queue.
   // the block's segment, XCD-major: blocks are dealt round-robin to the 8 XCDs, so block b (on XCD
@@ -229,27 +229,12 @@ void trace_kernel(KParams P) {
           }
           if (!found) break;
         }
-        } else {  // one shared queue (short units: DWork.n_segs = 0)
-          // the pool's bulk [0, q_bulk_end) in q_window-unit windows (few atomics on the one counter), its
-          // last units [q_bulk_end, n_units) from a second counter in 64-unit windows, so that no wave
-          // starts a long window at the pool's end (plan.h).  q_bulk_end is a multiple of q_window: a bulk
-          // window never straddles into the tail.  A wave whose bulk take comes back empty stays on the tail.
-          const unsigned long long bulk_end = kb->work.q_bulk_end;
-          nb = bulk_end;
-          if (!tail_mode) {
-            win = kb->work.q_window;
-            if (lane == 0) nb = atomicAdd(kb->unit_counter, (unsigned long long)win);
-            nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
-                 (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
-            tail_mode = nb >= bulk_end;
-          }
-          if (tail_mode) {
-            win = kSegmentWindow;
-            unsigned long long off = 0;
-            if (lane == 0) off = atomicAdd(kb->unit_counter + kTailCounter, (unsigned long long)win);
-            nb = bulk_end + (((unsigned long long)__builtin_amdgcn_readfirstlane((int)(off >> 32)) << 32) |
-                             (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)off));
-          }
+        } else {  // one shared queue (short units: DWork.n_segs = 0), q_window units per atomic (plan.h)
+          win = kb->work.q_window;
+          nb = 0;
+          if (lane == 0) nb = atomicAdd(kb->unit_counter, (unsigned long long)win);
+          nb = ((unsigned long long)__builtin_amdgcn_readfirstlane((int)(nb >> 32)) << 32) |
+               (unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)nb);
         }
         idx = (rank < avail) ? (w_next + rank) : (nb + (rank - avail));
         w_next = nb + (k - avail);
