@@ -25,8 +25,7 @@ def plan(tmp_path_factory):
     def run(*calls):
         args = [str(x) for call in calls for x in call]
         out = subprocess.run([exe] + args, check=True, capture_output=True, text=True, timeout=60).stdout.split("\n")
-        keys = ("chunk", "n_chunks", "per_pass", "passes", "partial_bytes", "segments", "ok", "queue_window",
-                "queue_tail", "bulk_end")
+        keys = ("chunk", "n_chunks", "per_pass", "passes", "partial_bytes", "segments", "ok", "queue_window")
         res = [dict(zip(keys, map(int, line.split()))) for line in out if line.strip()]
         return res if len(res) > 1 else res[0]
     return run
@@ -40,9 +39,8 @@ def test_headline_frame_one_pass(plan):
     # random_scene 1200x800 @ 500 spp: 8-sample units, one pass of 1.45 GB, per-block segments
     n = pixels(1200, 800)
     p = plan((n, 500, MEGA, LANES, 0, DEFAULT))
-    tail = LANES // 64 * 256
     assert p == dict(chunk=8, n_chunks=63, per_pass=63, passes=1, partial_bytes=n * 63 * 24, segments=1, ok=1,
-                     queue_window=256, queue_tail=tail, bulk_end=(n * 63 - tail) // 256 * 256)
+                     queue_window=256)
     assert p["partial_bytes"] == 1_451_520_000
 
 
@@ -139,28 +137,21 @@ def test_every_pass_fits_its_bound(plan):
             assert p["chunk"] <= 16
 
 
-def test_shared_queue_windows_shrink_for_the_pool_end(plan):
-    # one-sample units on the shared queue (cfg1 400x225 @ 50: 17 units per lane; the 8-rank share of the
-    # headline: 229): the pool's bulk in 256-unit windows (4 units per lane, one atomic per 256 units on the
-    # one counter — the 8-rank frame 24.1 -> 22.9 ms), its last round of them (256 units per resident wave,
-    # 1 M units on MI355X) from a second counter in 64-unit windows, so no wave starts a 4-unit-per-lane
-    # window at the pool's end (cfg1: 256-unit windows to the end ran 1490 Msamples/s, 64-unit windows 1830;
-    # gpurun_out/r05a, r05b)
+def test_shared_queue_window_follows_units_per_lane(plan):
+    # one-sample units on the shared queue: 256-unit windows (4 units per lane per atomic on the one
+    # counter) where a lane has >= 128 units — the 8-rank share of the headline (229 per lane: 24.1 -> 22.9
+    # ms against 64-unit windows) and its 8-rank sample share (227) —, else 64 — cfg1 400x225 @ 50 (17.7
+    # per lane: 1490 Msamples/s with 256-unit windows, 1830-1880 with 64; gpurun_out/r05a, r05f1), where
+    # 4-per-lane windows leave each wave too few tiles to average their cost over
     cfg1 = plan((pixels(400, 225), 50, MEGA, LANES, 0, DEFAULT))
-    r8 = plan((pixels(1200, 800) // 8, 500, MEGA, LANES, 0, DEFAULT))
-    tail = (LANES // 64) * 256
-    for p, n in ((cfg1, pixels(400, 225)), (r8, pixels(1200, 800) // 8)):
+    r8t = plan((pixels(1200, 800) // 8, 500, MEGA, LANES, 0, DEFAULT))
+    r8s = plan((pixels(1200, 800), 62, MEGA, LANES, 0, DEFAULT))
+    for p in (cfg1, r8t, r8s):
         assert p["segments"] == 0 and p["chunk"] == 1
-        assert p["queue_window"] == 256 and p["queue_tail"] == tail
-        units = n * p["per_pass"]
-        # the bulk ends on a window boundary (a bulk window never straddles into the tail) and leaves the
-        # tail, plus less than one window, to the second counter
-        assert p["bulk_end"] % 256 == 0 and tail <= units - p["bulk_end"] < tail + 256
-    # cfg1: 4.6 M units, the last 1 M (22 %) in 64-unit windows; the 8-rank share: 1.7 % of 60 M
-    assert 0.2 < (pixels(400, 225) * 50 - cfg1["bulk_end"]) / (pixels(400, 225) * 50) < 0.25
-    assert (pixels(1200, 800) // 8 * 500 - r8["bulk_end"]) / (pixels(1200, 800) // 8 * 500) < 0.02
-    # the tail scales with the resident waves; a pool no larger than the tail is all tail
-    small = plan((pixels(400, 225), 50, MEGA, 32 * 1024, 0, DEFAULT))
-    assert small["queue_tail"] == 512 * 256
-    tiny = plan((pixels(64, 64), 4, MEGA, LANES, 1, DEFAULT))
-    assert tiny["bulk_end"] == 0
+    assert cfg1["queue_window"] == 64 and r8t["queue_window"] == 256 and r8s["queue_window"] == 256
+    # the boundary: 128 units per resident lane
+    edge = 128 * LANES // 64  # pixels of 64-pixel tiles x 1 chunk
+    below, at = plan((edge - 64, 1, MEGA, LANES, 1, DEFAULT), (edge, 1, MEGA, LANES, 1, DEFAULT))
+    assert below["queue_window"] == 64 and at["queue_window"] == 64  # (1 chunk: 2 units per lane)
+    lo, hi = plan((pixels(1200, 800), 34, MEGA, LANES, 1, DEFAULT), (pixels(1200, 800), 35, MEGA, LANES, 1, DEFAULT))
+    assert (lo["queue_window"], hi["queue_window"]) == (64, 256)  # 960000 x 34 < 128 x 262144 <= 960000 x 35
