@@ -253,6 +253,15 @@ __device__ __forceinline__ bool slab_s(const double* b, v3 o, v3 inv, RaySigns n
   t_enter = t_min;
   return !(t_max <= t_min);
 }
+__device__ __forceinline__ bool slab_s(const double* b, v3 o, v3 inv, RaySigns ns, double t_min, double t_max,
+                                       double& t_enter, double& t_exit) {
+  slab_axis(b[0], b[3], ns.x, o.x, inv.x, t_min, t_max);
+  slab_axis(b[1], b[4], ns.y, o.y, inv.y, t_min, t_max);
+  slab_axis(b[2], b[5], ns.z, o.z, inv.z, t_min, t_max);
+  t_enter = t_min;
+  t_exit = t_max;
+  return !(t_max <= t_min);
+}
 
 // slab_s on a sphere's bounding box (c - r, c + r) (sphere.rs:54-60), with the near / far plane of
 // each axis formed as c + rn and c - rn, rn = (1/d < 0) ? r : -r: the same two sums slab_s selects
@@ -381,6 +390,53 @@ __device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, 
   if (rect_t<0, 2>(q, o, d, t_min, tc, t, inv, ok)) { tc = t; face = 5; }
   t_out = tc;
   return face;
+}
+
+// box_t in at most two passes of three faces (A/B switch RT_BOX_TWO_PASS; rejected: DESIGN.md §5 — +1 %
+// Cornell / final_scene, -0.7 % headline and cfg1 from the register pressure it adds to the leaf loop),
+// for rays whose every |d_i| is in face_div's range (no face quotient is NaN or infinite there).  The
+// sequential test keeps, of the faces whose rect test passes, the nearest — of equal t the last in face
+// order (each face meets the running closest with rect.rs:58's `t > t_max`).  A ray crosses each axis's two
+// planes in order: near (its entry side, the slab test's t0) and far (t1).  Pass 1 tests one plane of each
+// axis in face order (z, x, y: rising face index) — the near planes, or the far ones when the slab entry is
+// t_min (the origin is past every near plane) — and its result stands when the other set provably loses:
+//   * every far face quotient RN(num / d) >= the slab's RN(num * RN(1/d)) (1 - 3u) >= t_exit (1 - 3u), so
+//     a near result below RN(t_exit (1 - 2^-50)) beats each far face strictly;
+//   * with t_enter == t_min every near quotient is <= t_min (1 + 3.01u) (or <= 0), so a far result above
+//     RN(t_min (1 + 2^-50)) beats each near face strictly.
+// Else pass 2 tests the other set against pass 1's closest, and of a tie the higher face index wins — the
+// sequential result in every case (tests/box_pass_check.c: bit for bit on ~11 M adversarial draws).
+__device__ __forceinline__ int box_t2(const double* b, v3 o, v3 d, v3 inv, RaySigns ns, double t_min, double t_max,
+                                      double t_enter, double t_exit, double& t_out) {
+  const bool far_first = !(t_enter > t_min);
+  double tc = t_max, t1 = t_max;
+  int f1 = -1;
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool flip = far_first != (pass == 1);
+    double q[5], t;
+    int f = -1;
+    bool hi = ns.z != flip;  // the max-z plane: faces 0 (max) / 1 (min) of the xy sides
+    q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
+    q[4] = hi ? b[5] : b[2];
+    if (rect_t<0, 1>(q, o, d, t_min, tc, t, inv, true)) { tc = t; f = hi ? 0 : 1; }
+    hi = ns.x != flip;       // yz sides: faces 2 (max x) / 3 (min x)
+    q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
+    q[4] = hi ? b[3] : b[0];
+    if (rect_t<1, 2>(q, o, d, t_min, tc, t, inv, true)) { tc = t; f = hi ? 2 : 3; }
+    hi = ns.y != flip;       // xz sides: faces 4 (max y) / 5 (min y)
+    q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
+    q[4] = hi ? b[4] : b[1];
+    if (rect_t<0, 2>(q, o, d, t_min, tc, t, inv, true)) { tc = t; f = hi ? 4 : 5; }
+    if (pass == 0) {
+      t1 = tc; f1 = f;
+      if (f >= 0 && (far_first ? tc > t_min * (1.0 + 0x1p-50) : tc < t_exit * (1.0 - 0x1p-50))) break;
+    } else if (f >= 0 && (f1 < 0 || tc < t1 || f > f1)) {  // f >= 0: tc <= t1
+      t1 = tc; f1 = f;
+    }
+  }
+  t_out = t1;
+  return f1;
 }
 
 // ---- book-2 extensions (absent from the reference, parity unpinned) ----
@@ -1065,9 +1121,18 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
       continue;
     }
+#ifdef RT_BOX_TWO_PASS
+    double tx;
+    if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te, tx)) continue;  // a RectBox's bounding box is its p[0..5]
+#else
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
+#endif
     RT_STAT(++ptests);
+#ifdef RT_BOX_TWO_PASS
+    const int f = div_ok ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t) : box_t(pr.p, o, d, t_min, t_best, t);
+#else
     const int f = box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
+#endif
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
 #pragma unroll 1

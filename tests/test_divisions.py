@@ -33,3 +33,24 @@ def test_sphere_sure_pass_never_skips_a_rejecting_box_test(tmp_path):
     assert f["sure but box rejects"] == 0, r.stdout
     assert f["box rejects among them"] > 100000, r.stdout
     assert f["sure"] > 0.8 * f["sphere hits"], r.stdout
+
+
+def test_two_pass_rectbox_test_is_the_sequential_one(tmp_path):
+    """The megakernel tests a RectBox's near planes first and its far planes only when the margin does not
+    prove they lose (rt_device.h box_t2).  tests/box_pass_check.c compares it with the sequential six-face
+    test (rect.rs:132-156) on adversarial boxes and rays — edges, corners (faces tied at one t), grazing
+    rays, origins inside and on faces — bit for bit in (face, t).  Without the 2^-50 margins the same draws
+    give ~300 mismatches per million: the check has teeth."""
+    src = os.path.join(REPO, "tests", "box_pass_check.c")
+    for flags, want_bad in (([], False), (["-DNO_MARGIN"], True)):
+        exe = str(tmp_path / ("bpc" + "".join(flags)))
+        subprocess.run(["gcc", "-O2", "-ffp-contract=off", *flags, "-o", exe, src, "-lm"], check=True)
+        r = subprocess.run([exe, "3000000"], capture_output=True, text=True, timeout=120)
+        last = r.stdout.strip().split("\n")[-1].replace(",", "").split()
+        bad, compared, one_pass, ties = int(last[0]), int(last[2]), int(last[4]), int(last[7])
+        assert compared > 800000 and ties > 100000, r.stdout
+        if want_bad:
+            assert bad > 0, r.stdout
+        else:
+            assert r.returncode == 0 and bad == 0, r.stdout
+            assert one_pass > 0.8 * compared, r.stdout
