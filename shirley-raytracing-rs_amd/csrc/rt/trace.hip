@@ -66,7 +66,6 @@ void trace_kernel(KParams P) {
   unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;  // [stack_depth4][THREADS] packed entries
   stage_nodes4<MODE>(P.scene, lds_nodes, lds_prims);
 
-  const DScene& S = P.scene;
   const DCamera& C = P.cam;
   const DWork& W = P.work;
   const uint64_t seed = W.seed;
@@ -126,6 +125,10 @@ void trace_kernel(KParams P) {
 #if defined(RT_PHASE_TIMING) && !defined(RT_PHASE_NO_EVENTS)
     const unsigned long long ph_before = ph_lane_steps;
 #endif
+    // the scene record: book-2 instances read it with scalar loads from the pass's KBlock in each
+    // iteration, so its pointers are not held in SGPRs across the loop (the 768-thread instance's SGPR
+    // spills 50 -> 25, final_scene +0.2 %: DESIGN.md §5); reference scenes keep the kernel argument
+    const DScene& S = EXT ? *(const DScene*)&kblock(P.kconst)->scene : P.scene;
     // 1. one ray_color iteration (render.rs:30-46): closest hit and hit record, the material and the
     // texture leaf of a diffuse / emitting material
     bool hit = false, need_pn = false, need_r = false;
