@@ -644,29 +644,39 @@ __device__ __forceinline__ void prim_record(const DPrim& pr, int face, v3 o, v3 
 // as in the books' current edition).
 __device__ __forceinline__ Hit ext_record(const DExt* exts, const double* shutter, const DPrim pr, int face, v3 o,
                                        v3 d, double t, uint32_t pixel, uint32_t sample, uint64_t seed) {
+  // (each branch fills its own record, copied once: with the fields stored per branch the compiler kept
+  // u, v in scratch memory behind a select of their addresses — 2-4 scratch stores and 2 scratch loads
+  // per book-2 hit record)
   Hit h;
   const DExt& e = exts[pr.kind >> kPrimExtShift];
   const int32_t kind = pr.kind, base = kind & kPrimBaseMask;
   to_object(e, kind, o, d);
   if (kind & kPrimMedium) {
-    h.t = t;
-    h.point = o + scale(d, t);
-    h.normal = V(1.0, 0.0, 0.0);
-    h.front_face = true;
-    h.u = h.v = 0.0;
+    Hit m;
+    m.t = t;
+    m.point = o + scale(d, t);
+    m.normal = V(1.0, 0.0, 0.0);
+    m.front_face = true;
+    m.u = 0.0;
+    m.v = 0.0;
+    h = m;
   } else if (base == kPrimMovingSphere) {
     const v3 c = moving_center(pr, e, ray_time(shutter, pixel, sample, seed));
-    h.t = t;
-    h.point = o + scale(d, t);
-    const v3 n = scale(h.point - c, pr.p[4]);  // p[4] = 1.0 / r (host)
+    Hit m;
+    m.t = t;
+    m.point = o + scale(d, t);
+    const v3 n = scale(m.point - c, pr.p[4]);  // p[4] = 1.0 / r (host)
     const UV uv = sphere_uv(n.x, n.y, n.z);
-    h.u = uv.u;
-    h.v = uv.v;
-    finish_hit(h, d, n);
+    m.u = uv.u;
+    m.v = uv.v;
+    finish_hit(m, d, n);
+    h = m;
   } else {
     DPrim q = pr;
     q.kind = base;
-    prim_record<true>(q, face, o, d, t, h);
+    Hit m;
+    prim_record<true>(q, face, o, d, t, m);
+    h = m;
   }
   if (kind & kPrimXform) {
     const v3 p = h.point, n = h.normal;
