@@ -392,8 +392,12 @@ __device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, 
   return face;
 }
 
-// box_t in at most two passes of three faces (A/B switch RT_BOX_TWO_PASS; rejected: DESIGN.md §5 — +1 %
-// Cornell / final_scene, -0.7 % headline and cfg1 from the register pressure it adds to the leaf loop),
+#ifndef RT_BOX_TWO_PASS
+#define RT_BOX_TWO_PASS 2  // book-2 instances only
+#endif
+// box_t in at most two passes of three faces (RT_BOX_TWO_PASS: the book-2 instances, final_scene +1 %; in
+// the reference-scene instance +1 % Cornell but -0.7 % headline and cfg1 from the register pressure it
+// adds to the leaf loop: DESIGN.md §5),
 // for rays whose every |d_i| is in face_div's range (no face quotient is NaN or infinite there).  The
 // sequential test keeps, of the faces whose rect test passes, the nearest — of equal t the last in face
 // order (each face meets the running closest with rect.rs:58's `t > t_max`).  A ray crosses each axis's two
@@ -1131,18 +1135,14 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
       continue;
     }
-#ifdef RT_BOX_TWO_PASS
+    // the two-pass face test (box_t2) in the instances named by RT_BOX_TWO_PASS: 1 reference scenes, 2 book-2
+    // scenes, 3 both
+    constexpr bool kTwoPass = (RT_BOX_TWO_PASS & (EXT ? 2 : 1)) != 0;
     double tx;
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te, tx)) continue;  // a RectBox's bounding box is its p[0..5]
-#else
-    if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te)) continue;  // a RectBox's bounding box is its p[0..5]
-#endif
     RT_STAT(++ptests);
-#ifdef RT_BOX_TWO_PASS
-    const int f = div_ok ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t) : box_t(pr.p, o, d, t_min, t_best, t);
-#else
-    const int f = box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
-#endif
+    const int f = (kTwoPass && div_ok) ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
+                                       : box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
 #pragma unroll 1
