@@ -45,11 +45,15 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 #ifndef RT_KSCENE
 #define RT_KSCENE 1
 #endif
-// Minimum waves per SIMD of the 256-thread instances (4 = 128 VGPRs: 3 and 5 measured slower).
+// Minimum waves per SIMD of the 256-thread instances (4 = 128 VGPRs: 3 and 5 measured slower);
+// the book-2 ones at 3 (168 VGPRs: ~90 spilled VGPRs at 4; final_scene on them +27 %).
 constexpr int kNarrowWaves = 4;
+#ifndef RT_NARROW_WAVES_EXT
+#define RT_NARROW_WAVES_EXT 3
+#endif
 
 template <int THREADS, int MODE, bool EXT>
-__global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : kNarrowWaves)
+__global__ __launch_bounds__(THREADS, THREADS >= kTraceThreadsWide3 ? 1 : (EXT ? RT_NARROW_WAVES_EXT : kNarrowWaves))
 void trace_kernel(KParams P) {
   extern __shared__ unsigned char lds_raw[];
   const int tid = threadIdx.x;
