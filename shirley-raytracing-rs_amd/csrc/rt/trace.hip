@@ -47,7 +47,10 @@ __host__ __device__ inline size_t lds_bytes(int n_lds_nodes, int stack_depth, in
 #endif
 // Minimum waves per SIMD of the 256-thread instances (4 = 128 VGPRs: 3 and 5 measured slower);
 // the book-2 ones at 3 (168 VGPRs: ~90 spilled VGPRs at 4; final_scene on them +27 %).
-constexpr int kNarrowWaves = 4;
+#ifndef RT_NARROW_WAVES
+#define RT_NARROW_WAVES 4
+#endif
+constexpr int kNarrowWaves = RT_NARROW_WAVES;
 #ifndef RT_NARROW_WAVES_EXT
 #define RT_NARROW_WAVES_EXT 3
 #endif

@@ -92,7 +92,7 @@ SCENES = [("random", 48, "std16x9"), ("random-night", 48, "std16x9"), ("demo", 4
           ("perlin", 48, "std16x9"), ("earth", 48, "square"), ("box-light", 48, "std16x9"),
           ("cornell", 40, "square"),
           # book-2 extensions (absent from the reference; oracle restatement, parity unpinned):
-          # reduced final scene (whole scene in LDS) and the full one (1409 objects, tree via L1/L2)
+          # reduced final scene (whole scene in LDS) and the full one (1409 objects, nodes in LDS)
           ("final:6:60", 40, "square"), ("final", 32, "square")]
 
 
@@ -580,8 +580,8 @@ def test_max_depth_zero_partial_units(gpu):
 
 
 def test_final_scene_tile_sharded_world8(gpu):
-    """BASELINE config 5's data path on one device: book-2 final_scene (1409 objects, EXT kernels,
-    tree via L1/L2) rendered as the 8 ranks' interleaved tiles (rt_render_tiles_device), gathered
+    """BASELINE config 5's data path on one device: book-2 final_scene (1409 objects, EXT kernels; its
+    4-wide tree in the 768-thread block's LDS since the cluster is flattened) rendered as the 8 ranks' interleaved tiles (rt_render_tiles_device), gathered
     rank-major and scattered back (rt_unpack_tiles_device): bit-identical to the full frame."""
     import torch
     spp, world = 3, 8
@@ -617,3 +617,24 @@ def test_gen_spheres_side11_matches_oracle(gpu, bvh):
     img = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
     check_parity(img, ora, spp, frac_exact=exact_floor("spheres"))
+
+
+def test_final_scene_on_the_narrow_block(gpu, monkeypatch):
+    """The book-2 256-thread instances (a book-2 scene whose tree does not fit the wide block's LDS; 3 waves
+    per SIMD, trace.hip RT_NARROW_WAVES_EXT): final_scene forced onto them (SHIRLEY_NO_WIDE, read at upload)
+    renders the wide block's frame bit for bit, and the oracle's within the parity rule."""
+    spp = 4
+    scene = rt.scenes.final_scene(SEED).finalize(SEED)
+    cam = rt.scene_camera("final", 32, "square")
+    gpu.upload(scene)
+    assert gpu.stats().wide_block == 1
+    wide = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
+    monkeypatch.setenv("SHIRLEY_NO_WIDE", "1")
+    gpu.upload(scene)
+    assert gpu.stats().wide_block == 0
+    narrow = gpu.render(cam, rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp))
+    monkeypatch.delenv("SHIRLEY_NO_WIDE")
+    gpu.upload(scene)  # (the next test's device: the default block again)
+    assert np.array_equal(narrow, wide)
+    ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
+    check_parity(narrow, ora, spp, frac_exact=exact_floor("final"))
