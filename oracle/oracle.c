@@ -23,6 +23,23 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* The transcendental functions: glibc's (the reference's libm), or (OR_PORTABLE_LIBM, the diagnostic build
+ * liboracle_pl.so) the portable ones the kernel's RT_PORTABLE_LIBM build also calls. */
+#ifdef OR_PORTABLE_LIBM
+#include "portable_libm.h"
+#define OR_SIN pl_sin
+#define OR_LOG pl_log
+#define OR_ACOS pl_acos
+#define OR_ATAN2 pl_atan2
+#define OR_POW5(x) pl_pow5(x)
+#else
+#define OR_SIN sin
+#define OR_LOG log
+#define OR_ACOS acos
+#define OR_ATAN2 atan2
+#define OR_POW5(x) pow(x, 5.0)
+#endif
+
 /* ------------------------------------------------------------------------------------------ */
 /* RNG                                                                                          */
 /* ------------------------------------------------------------------------------------------ */
@@ -244,8 +261,8 @@ static int sphere_hit(const double* p, const ray_t* r, double t_min, double t_ma
   OR_SPHERE_STAT(2, oc, r->d, half_b, cc, radius, disc);
   v3 point = ray_at(r, root);
   v3 normal = vscale(vsub(point, c), 1.0 / radius);
-  double theta = acos(-normal.y);
-  double phi = atan2(-normal.z, normal.x) + PI_;
+  double theta = OR_ACOS(-normal.y);
+  double phi = OR_ATAN2(-normal.z, normal.x) + PI_;
   double u = phi / (2.0 * PI_);
   double v = theta / PI_;
   *out = make_hit(r, point, normal, root, u, v);
@@ -354,7 +371,7 @@ static int medium_hit(const rt_object* o, int32_t obj, const ray_t* r, double t_
   double ray_length = vlen(r->d);
   double distance_inside_boundary = (rec2.t - rec1.t) * ray_length;
   double neg_inv_density = -1.0 / o->density;
-  double hit_distance = neg_inv_density * log(side_draw(cx->seed, cx->draw, cx->sample, cx->pixel,
+  double hit_distance = neg_inv_density * OR_LOG(side_draw(cx->seed, cx->draw, cx->sample, cx->pixel,
                                                         STREAM_MEDIUM | (uint32_t)obj));
   if (hit_distance > distance_inside_boundary) return 0;
   double t = rec1.t + hit_distance / ray_length;
@@ -842,7 +859,7 @@ static v3 texture_value(const or_scene* s, int32_t ti, double u, double v, v3 p)
       case RT_TEX_SOLID: /* solid.rs:17-21 */
         return V(t->color[0], t->color[1], t->color[2]);
       case RT_TEX_CHECKER: { /* checker.rs:27-37 */
-        double sines = sin(t->scale * p.x) * sin(t->scale * p.y) * sin(t->scale * p.z);
+        double sines = OR_SIN(t->scale * p.x) * OR_SIN(t->scale * p.y) * OR_SIN(t->scale * p.z);
         ti = (sines < 0.0) ? t->odd : t->even;
         continue;
       }
@@ -852,7 +869,7 @@ static v3 texture_value(const or_scene* s, int32_t ti, double u, double v, v3 p)
         v3 dimm_scale = V(1.0 / 5.0, 1.0 / 10.0, 1.0);
         v3 dimm_weight = vunit(V(0.0, 0.0, 1.0));
         v3 vd = vmul(vscale(dimm_scale, t->scale), p);
-        vd = V(sin(vd.x + turb), sin(vd.y + turb), sin(vd.z + turb));
+        vd = V(OR_SIN(vd.x + turb), OR_SIN(vd.y + turb), OR_SIN(vd.z + turb));
         double total_noise = vdot(vd, dimm_weight);
         double noise = 0.5 * (1.0 + total_noise);
         return vscale(V(1.0, 1.0, 1.0), noise);
@@ -879,7 +896,7 @@ static v3 texture_value(const or_scene* s, int32_t ti, double u, double v, v3 p)
 static double reflectance(double cosine, double ref_idx) {
   double r0 = (1.0 - ref_idx) / (1.0 + ref_idx);
   r0 = r0 * r0;
-  return r0 + (1.0 - r0) * pow(1.0 - cosine, 5.0);
+  return r0 + (1.0 - r0) * OR_POW5(1.0 - cosine);
 }
 
 /* emitted: lighting.rs:21-24 (DiffuseLight), 59-66 (FairyLight); default None (mod.rs:22-24) */

@@ -3,6 +3,23 @@
 // intersection, BVH traversal, textures, materials, camera.  Semantics follow the reference line by
 // line (citations inline); compiled with -ffp-contract=off (Rust never fuses a*b+c).
 #pragma once
+
+// The transcendental functions of the path: the device libm, or (RT_PORTABLE_LIBM, a diagnostic build
+// only) portable_libm.h's, which the oracle's OR_PORTABLE_LIBM build shares
+#ifdef RT_PORTABLE_LIBM
+#include "portable_libm.h"
+#define RT_SIN pl_sin
+#define RT_LOG pl_log
+#define RT_ACOS pl_acos
+#define RT_ATAN2 pl_atan2
+#define RT_POW5_LIBM(x) pl_pow5(x)
+#else
+#define RT_SIN sin
+#define RT_LOG log
+#define RT_ACOS acos
+#define RT_ATAN2 atan2
+#define RT_POW5_LIBM(x) pow(x, 5.0)
+#endif
 #include <hip/hip_runtime.h>
 
 #include "../../../include/shirley_rt.h"
@@ -541,7 +558,7 @@ __device__ __forceinline__ ExtHit ext_t(const DExt* exts, const double* shutter,
   if (t1 < 0.0) t1 = 0.0;
   const double ray_length = len(d);
   const double inside = (t2 - t1) * ray_length;
-  const double hd = e.neg_inv_density * log(side_draw(seed, draw, sample, pixel, kStreamMedium | (uint32_t)prim));
+  const double hd = e.neg_inv_density * RT_LOG(side_draw(seed, draw, sample, pixel, kStreamMedium | (uint32_t)prim));
   if (hd > inside) return r;
   const double th = t1 + hd / ray_length;
   if (th > t_max) return r;
@@ -594,8 +611,8 @@ struct UV {
   double u, v;
 };
 __device__ __noinline__ UV sphere_uv(double nx, double ny, double nz) {
-  double theta = acos(-ny);
-  double phi = atan2(-nz, nx) + 3.14159265358979323846;
+  double theta = RT_ACOS(-ny);
+  double phi = RT_ATAN2(-nz, nx) + 3.14159265358979323846;
   return UV{phi / (2.0 * 3.14159265358979323846), theta / 3.14159265358979323846};
 }
 
@@ -1456,7 +1473,7 @@ __device__ __forceinline__ double marble_t(TP T, double sc, v3 p) {
     tp = scale(tp, 2.0);
   }
   double turb = 10.0 * fabs(accum);
-  double total_noise = sin(sc * p.z + turb);
+  double total_noise = RT_SIN(sc * p.z + turb);
   return 0.5 * (1.0 + total_noise);
 }
 
@@ -1540,7 +1557,7 @@ __device__ __forceinline__ double marble_coop(TP tables, bool need, int tab, dou
   }
   const double turb = 10.0 * fabs(accum);
   if (need) PH_COUNT(14);
-  return need ? 0.5 * (1.0 + sin(sc * p.z + turb)) : 0.0;
+  return need ? 0.5 * (1.0 + RT_SIN(sc * p.z + turb)) : 0.0;
 }
 
 // One Philox block of a lane's stream: draws 2c (c0, c1) and 2c + 1 (c2, c3) of (seed, pixel, sample).
@@ -1827,7 +1844,7 @@ __device__ __forceinline__ void camera_ray_drawn(const CAM& C, double x, double 
 
 // checker.rs:28-30
 __device__ __noinline__ double checker_sines(double s, double x, double y, double z) {
-  return sin(s * x) * sin(s * y) * sin(s * z);
+  return RT_SIN(s * x) * RT_SIN(s * y) * RT_SIN(s * z);
 }
 
 // Sign of sin(y) for a double y, exactly: +1, -1 or 0 — or 2 when this fast path does not decide
@@ -1935,7 +1952,7 @@ __device__ __forceinline__ v3 texture_value(const DScene& S, const DPerlin* lds_
 // rounded save for values within 2^-100 of a rounding boundary — as glibc's pow(x, 5.0) is (the
 // oracle's and the reference's libm).  Other x take pow().
 __device__ __forceinline__ double pow5(double x) {
-  if (!(x >= 0.0 && x <= 4.0)) return pow(x, 5.0);
+  if (!(x >= 0.0 && x <= 4.0)) return RT_POW5_LIBM(x);
   const double x2 = x * x;
   const double x2l = fma(x, x, -x2);
   const double x4 = x2 * x2;
@@ -1953,7 +1970,7 @@ __device__ __forceinline__ double reflectance_inl(double cosine, double ref_idx)
 }
 __device__ __noinline__ double reflectance(double cosine, double ref_idx) { return reflectance_inl(cosine, ref_idx); }
 // reflectance_inl with its r0^2 from the host (DMat: a dielectric's albedo[0] / albedo[1] for the front / back face)
-__device__ __noinline__ double pow5_libm(double x) { return pow(x, 5.0); }
+__device__ __noinline__ double pow5_libm(double x) { return RT_POW5_LIBM(x); }
 __device__ __forceinline__ double reflectance_r0sq(double cosine, double r0sq) {
   const double x = 1.0 - cosine;
   double p;

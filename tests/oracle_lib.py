@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(REPO, "shirley-raytracing-rs_amd"))
 from raytracer import _native as N  # noqa: E402
 
 ORACLE_DIR = os.path.join(REPO, "oracle")
-ORACLE_SO = os.path.join(ORACLE_DIR, "liboracle.so")
+ORACLE_SO = os.environ.get("SHIRLEY_ORACLE_SO") or os.path.join(ORACLE_DIR, "liboracle.so")  # (libm isolation: liboracle_pl.so)
 
 _d6 = C.c_double * 6
 
