@@ -54,3 +54,15 @@ def test_two_pass_rectbox_test_is_the_sequential_one(tmp_path):
         else:
             assert r.returncode == 0 and bad == 0, r.stdout
             assert one_pass > 0.8 * compared, r.stdout
+
+
+def test_portable_libm_is_accurate(tmp_path):
+    """The diagnostic libm shared by the RT_PORTABLE_LIBM kernels and the OR_PORTABLE_LIBM oracle
+    (csrc/rt/portable_libm.h) is within a few ulps of glibc: its frames are plausible images, so their
+    bit-identity (tests/test_gpu_libm_isolation.py) is a test of the path, not of a degenerate function."""
+    exe = str(tmp_path / "plcheck")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-I", os.path.join(REPO, "shirley-raytracing-rs_amd", "csrc", "rt"),
+                    "-o", exe, os.path.join(REPO, "tools", "portable_libm_check.c"), "-lm"], check=True)
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=120, check=True).stdout.split()
+    vals = [float(out[out.index(k) + 1]) for k in ("sin", "log", "atan2", "acos")]
+    assert all(v <= 1e-15 for v in vals), out
