@@ -553,6 +553,8 @@ def main():
                      "traffic": traffic,
                      "kernel": "trace_kernel", "kernel_ms": round(k_ms, 3), "launches_per_step": launches,
                      "bytes_per_segment": BYTES_PER_SEGMENT, "segments_per_launch": int(seg),
+                     # SURVEY.md §8d's third figure: path segments per second of the trace kernel
+                     "segments_per_s": round(seg / (k_ms * 1e-3), 1) if traced else None,
                      "f64_state": {"bytes_per_segment": BYTES_PER_SEGMENT_F64,
                                    "achieved": round(achieved_f64, 2) if traced else None,
                                    "frac": round(achieved_f64 / HBM_PEAK_GBS, 5) if traced else None},
