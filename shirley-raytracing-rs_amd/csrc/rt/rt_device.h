@@ -1124,9 +1124,6 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     // primitive is re-read for it, so no copy of c, r is held across the sphere test.
     bool sure;
     if (!sphere_t_sure(pr.p, o, d, ra, ra_ok, t_min, t_best, t, sure)) continue;
-#ifdef RT_SURE_LDS_ONLY  // (A/B: the sure-pass only where the scene is LDS-resident)
-    if (MODE != kSceneLds) sure = false;
-#endif
     if (!sure) {
       const DPrim* pp = &pr;
       asm volatile("" : "+v"(pp));
