@@ -435,6 +435,9 @@ __global__ __launch_bounds__(256) void reduce_kernel(const double* __restrict__ 
     b = out[o + 2];
   }
   if (inside) {
+    // (unrolled: the loads of 8 chunks in flight at once — a sharded frame's reduce runs few waves per
+    // CU over many chunks; the additions stay in chunk order)
+#pragma unroll 8
     for (int c = 0; c < n_chunks; ++c) {
       const double* p = partial + ((long long)c * n_pix + i) * 3;
       r += p[0];
