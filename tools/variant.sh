@@ -12,8 +12,8 @@ rm -rf "$tmp" && mkdir -p "$tmp"
 cp -r "$src"/csrc "$src"/Makefile "$tmp"/
 mkdir -p "$tmp/../include" 2>/dev/null || true
 cp -r include "$tmp/../" 2>/dev/null || true
-make -C "$tmp" -j8 lib/libshirley_rt.so \
-  HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function ${LICM_FLAG--mllvm -disable-machine-licm} ${TRK_FLAG-} $*" >/dev/null
+make -C "$tmp" -j8 lib/libshirley_rt.so ARCH="${ARCH:-gfx950}" \
+  HIPFLAGS="--offload-arch=${ARCH:-gfx950} -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function ${LICM_FLAG--mllvm -disable-machine-licm} ${TRK_FLAG-} $*" >/dev/null
 mkdir -p exp/$name
 cp "$tmp/lib/libshirley_rt.so" exp/$name/
 cp shirley-raytracing-rs_amd/lib/libshirley_host.so exp/$name/
