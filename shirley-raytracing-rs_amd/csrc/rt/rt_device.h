@@ -410,11 +410,11 @@ __device__ __forceinline__ int box_t(const double* b, v3 o, v3 d, double t_min, 
 }
 
 #ifndef RT_BOX_TWO_PASS
-#define RT_BOX_TWO_PASS 2  // book-2 instances only
+#define RT_BOX_TWO_PASS 6  // book-2 instances: box_t2; reference scenes: box_t1f
 #endif
 // box_t in at most two passes of three faces (RT_BOX_TWO_PASS: the book-2 instances, final_scene +1 %; in
 // the reference-scene instance +1 % Cornell but -0.7 % headline and cfg1 from the register pressure it
-// adds to the leaf loop: DESIGN.md §5),
+// adds to the leaf loop, where box_t1f below wins instead: DESIGN.md §5),
 // for rays whose every |d_i| is in face_div's range (no face quotient is NaN or infinite there).  The
 // sequential test keeps, of the faces whose rect test passes, the nearest — of equal t the last in face
 // order (each face meets the running closest with rect.rs:58's `t > t_max`).  A ray crosses each axis's two
@@ -458,6 +458,32 @@ __device__ __forceinline__ int box_t2(const double* b, v3 o, v3 d, v3 inv, RaySi
   }
   t_out = t1;
   return f1;
+}
+
+// box_t2's first pass alone, falling back to the six-face sequence wherever the margin does not prove it
+// (RT_BOX_TWO_PASS & 4: the reference-scene instance) — the same result, fewer values held across the
+// fallback than box_t2's merge of two passes
+__device__ __forceinline__ int box_t1f(const double* b, v3 o, v3 d, v3 inv, RaySigns ns, double t_min, double t_max,
+                                       double t_enter, double t_exit, double& t_out) {
+  const bool far_first = !(t_enter > t_min);
+  double tc = t_max, q[5], t;
+  int f = -1;
+  bool hi = ns.z != far_first;
+  q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
+  q[4] = hi ? b[5] : b[2];
+  if (rect_t<0, 1>(q, o, d, t_min, tc, t, inv, true)) { tc = t; f = hi ? 0 : 1; }
+  hi = ns.x != far_first;
+  q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
+  q[4] = hi ? b[3] : b[0];
+  if (rect_t<1, 2>(q, o, d, t_min, tc, t, inv, true)) { tc = t; f = hi ? 2 : 3; }
+  hi = ns.y != far_first;
+  q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
+  q[4] = hi ? b[4] : b[1];
+  if (rect_t<0, 2>(q, o, d, t_min, tc, t, inv, true)) { tc = t; f = hi ? 4 : 5; }
+  if (!(f >= 0 && (far_first ? tc > t_min * (1.0 + 0x1p-50) : tc < t_exit * (1.0 - 0x1p-50))))
+    f = box_t(b, o, d, t_min, t_max, tc, inv, true);
+  t_out = tc;
+  return f;
 }
 
 // ---- book-2 extensions (absent from the reference, parity unpinned) ----
@@ -1149,14 +1175,16 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
       continue;
     }
-    // the two-pass face test (box_t2) in the instances named by RT_BOX_TWO_PASS: 1 reference scenes, 2 book-2
-    // scenes, 3 both
+    // RT_BOX_TWO_PASS bits: box_t2 in the reference-scene (1) / book-2 (2) instances, box_t1f in the
+    // reference-scene (4) / book-2 (8) ones, else the six-face sequence
     constexpr bool kTwoPass = (RT_BOX_TWO_PASS & (EXT ? 2 : 1)) != 0;
+    constexpr bool kOneFull = (RT_BOX_TWO_PASS & (EXT ? 8 : 4)) != 0;
     double tx;
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te, tx)) continue;  // a RectBox's bounding box is its p[0..5]
     RT_STAT(++ptests);
-    const int f = (kTwoPass && div_ok) ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
-                                       : box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
+    const int f = (kTwoPass && div_ok)   ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
+                  : (kOneFull && div_ok) ? box_t1f(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
+                                         : box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
     if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
 #pragma unroll 1

@@ -1,4 +1,4 @@
-/* CPU check of the megakernel's two-pass RectBox test (rt_device.h box_t2) against the sequential six-face
+/* CPU check of the megakernel's two-pass RectBox tests (rt_device.h box_t2, box_t1f) against the sequential six-face
  * test (box_t, rect.rs:132-156): the same IEEE binary64 operations (gcc -ffp-contract=off; the device's
  * face_div is the correctly rounded quotient, as `/` here; the slab test multiplies by RN(1/d)).
  * Adversarial draws: boxes from unit cubes to slabs 1e-9 thin and far from the origin, rays aimed at face
@@ -106,6 +106,30 @@ static int box_t2(const double* b, v3 o, v3 d, v3 inv, double t_min, double t_ma
   return f1;
 }
 
+/* rt_device.h box_t1f: box_t2's first pass, else the six-face sequence */
+static int box_t1f(const double* b, v3 o, v3 d, v3 inv, double t_min, double t_max, double t_enter, double t_exit,
+                   double* t_out) {
+  const int nz = inv.z < 0.0, nx = inv.x < 0.0, ny = inv.y < 0.0;
+  const int far_first = !(t_enter > t_min);
+  double q[5], t, tc = t_max;
+  int f = -1, hi = nz != far_first;
+  q[0] = b[0]; q[1] = b[3]; q[2] = b[1]; q[3] = b[4];
+  q[4] = hi ? b[5] : b[2];
+  if (rect_t(0, 1, q, o, d, t_min, tc, &t)) { tc = t; f = hi ? 0 : 1; }
+  hi = nx != far_first;
+  q[0] = b[1]; q[1] = b[4]; q[2] = b[2]; q[3] = b[5];
+  q[4] = hi ? b[3] : b[0];
+  if (rect_t(1, 2, q, o, d, t_min, tc, &t)) { tc = t; f = hi ? 2 : 3; }
+  hi = ny != far_first;
+  q[0] = b[0]; q[1] = b[3]; q[2] = b[2]; q[3] = b[5];
+  q[4] = hi ? b[4] : b[1];
+  if (rect_t(0, 2, q, o, d, t_min, tc, &t)) { tc = t; f = hi ? 4 : 5; }
+  if (!(f >= 0 && (far_first ? tc > t_min * (1.0 + MARGIN) : tc < t_exit * (1.0 - MARGIN))))
+    f = box_t(b, o, d, t_min, t_max, &tc);
+  *t_out = tc;
+  return f;
+}
+
 /* a point on the box: interior of a face, an edge, or a corner */
 static v3 box_point(const double* b, int kind) {
   double p[3];
@@ -174,6 +198,12 @@ int main(int argc, char** argv) {
         double q[5] = {b[D1], b[D1 + 3], b[D2], b[D2 + 3], b[(3 - D1 - D2) + ((k & 1) ? 0 : 3)]};
         if (rect_t(D1, D2, q, o, d, t_min, t_max, &tt) && tt == ta) { ++ties; break; }
       }
+    }
+    double tf;
+    const int ff = box_t1f(b, o, d, inv, t_min, t_max, te, tx, &tf);
+    if (ff != fa || (fa >= 0 && tf != ta)) {
+      if (bad < 5) printf("box_t1f mismatch: face %d/%d t %a/%a\n", fa, ff, ta, tf);
+      ++bad;
     }
     if (fa != fb || (fa >= 0 && ta != tb)) {
       if (bad < 5)

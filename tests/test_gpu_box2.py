@@ -3,7 +3,8 @@ adversarial rays at a RectBox — aimed at its faces, edges and corners (where f
 t, and entry meets exit), from outside, from inside and from points on its faces — traced through the
 book-2 kernel instance (the scene holds a moving sphere, so the render traversal runs leaf_tests4<EXT>)
 must return the oracle's sequential six-face record (rect.rs:132-156) bit for bit, and the same record as
-the reference-scene instance (six faces in sequence) on the scene without the moving sphere.
+the reference-scene instance (box_t1f: the entry planes, else the six-face sequence) on the scene without
+the moving sphere.
 tests/box_pass_check.c proves the same on the CPU over ~11 M draws."""
 import numpy as np
 import pytest
