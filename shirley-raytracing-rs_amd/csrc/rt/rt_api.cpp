@@ -23,7 +23,7 @@
 
 namespace rt {
 size_t trace_lds_bytes(int n_lds_nodes4, int node4_size, int n_lds_prims, int n_lds_perlin, int stack_depth4,
-                       int threads);
+                       int threads, int n_lds_mats, int n_lds_texs);
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu);
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream);
 bool split_supported_nt(int nt);
@@ -1046,7 +1046,9 @@ int render_window(rt_ctx* c, const rt_camera* cam, const rt_render_params* p, co
       if (st) return st;
     } else if (engine == RT_ENGINE_SPLIT) {
       kp.split_refill = c->split_refill;
-      HIP_TRY(c, launch_split(kp, c->split_nt, c->cu_count, s));
+      KParams ks = kp;  // (the split engine's LDS layout holds no material tables)
+      ks.scene.n_lds_mats = ks.scene.n_lds_texs = 0;
+      HIP_TRY(c, launch_split(ks, c->split_nt, c->cu_count, s));
     } else {
       HIP_TRY(c, launch_trace(kp, (int)nseg, c->mk_threads, s));
     }
@@ -1345,6 +1347,18 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
                                   (long long)d->n_perlin * (long long)sizeof(DPerlin) <= kLdsBytes &&
                           !getenv("SHIRLEY_NO_LDS_PERLIN");
   S.n_lds_perlin = perlin_lds ? d->n_perlin : 0;
+  // and the material and texture tables (the record / shading reads: headline +1.0 %, Cornell +0.7 %,
+  // DESIGN.md §5; SHIRLEY_NO_LDS_MATS: tuning switch).  The wavefront and split engines keep their own
+  // LDS layouts and read them from global memory (their scene copies carry n_lds_mats = 0).
+  S.n_lds_mats = S.n_lds_texs = 0;
+  if (prims_lds && (d->n_perlin == 0 || perlin_lds) && !getenv("SHIRLEY_NO_LDS_MATS") &&
+      wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) +
+              (long long)S.n_lds_perlin * (long long)sizeof(DPerlin) +
+              (long long)mats.size() * (long long)sizeof(DMat) + (long long)texs.size() * (long long)sizeof(DTex) <=
+          kLdsBytes) {
+    S.n_lds_mats = (int32_t)mats.size();
+    S.n_lds_texs = (int32_t)texs.size();
+  }
 
   int bpc = 0;
   HIP_TRY(c, trace_occupancy(S, c->mk_threads, &bpc));
@@ -1353,6 +1367,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
 
   // wavefront extend block: its own (larger) stack area, the rest of LDS for nodes
   DScene W = S;
+  W.n_lds_mats = W.n_lds_texs = 0;
   long long wf_stack = (long long)S.stack_depth * wf_extend_threads() * 8;
   if (wf_stack > kLdsBytes)
     return fail(c, RT_E_UNSUPPORTED, "BVH too deep for the LDS traversal stack (depth %d)", depth);
@@ -1368,7 +1383,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
     if (b4 >= 1) {
       c->wf_wide = true;
       c->wf4_blocks_per_cu = b4;
-      c->wf_scene = S;  // wf_extend4 reads the megakernel's LDS layout
+      c->wf_scene = S;  // wf_extend4 reads the megakernel's LDS layout (without the material tables)
+      c->wf_scene.n_lds_mats = c->wf_scene.n_lds_texs = 0;
     }
   }
   c->n_perlin = d->n_perlin;

@@ -1413,6 +1413,17 @@ __device__ __forceinline__ void stage_nodes4(const DScene& S, N4* lds_nodes, DPr
     int4* td = reinterpret_cast<int4*>(lds_prims + S.n_lds_prims);
     const int t16 = S.n_lds_perlin * (int)(sizeof(DPerlin) / 16);
     for (int i = threadIdx.x; i < t16; i += blockDim.x) td[i] = ts[i];
+    // then the material and texture tables (when they fit: S.n_lds_mats > 0)
+    if (S.n_lds_mats > 0) {
+      const int4* ms = reinterpret_cast<const int4*>(S.mats);
+      int4* md = td + t16;
+      const int m16 = S.n_lds_mats * (int)(sizeof(DMat) / 16);
+      for (int i = threadIdx.x; i < m16; i += blockDim.x) md[i] = ms[i];
+      const int4* xs = reinterpret_cast<const int4*>(S.texs);
+      int4* xd = md + m16;
+      const int x16 = S.n_lds_texs * (int)(sizeof(DTex) / 16);
+      for (int i = threadIdx.x; i < x16; i += blockDim.x) xd[i] = xs[i];
+    }
   }
   __syncthreads();
 }
@@ -1902,14 +1913,16 @@ __device__ __forceinline__ bool checker_odd(double s, double x, double y, double
 
 // The texture a material reads, resolved down to its leaf (checker.rs:27-37 picks odd/even by the
 // sign of a sine product).  Returns the leaf index.
-__device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) {
+__device__ __forceinline__ int resolve_texture_t(const DTex* texs, int ti, v3 p) {
   for (;;) {
-    const DTex& t = S.texs[ti];
+    const DTex& t = texs[ti];
     if (t.kind != RT_TEX_CHECKER) return ti;
     PH_COUNT(16);
     ti = checker_odd(t.scale, p.x, p.y, p.z) ? t.odd : t.even;
   }
 }
+
+__device__ __forceinline__ int resolve_texture(const DScene& S, int ti, v3 p) { return resolve_texture_t(S.texs, ti, p); }
 
 // image_texture.rs:34-56: clamp, flip v, truncate, /255.
 __device__ __forceinline__ v3 image_texel(const DTex& tx, double u, double v) {
@@ -1948,9 +1961,9 @@ __device__ __forceinline__ UV hit_uv(const DPrim& pr, int face, const Hit& h) {
 // Texture value at a hit (texture.rs Texture::value): checker resolved by the hit point, Perlin
 // marble by the hit point, solid directly, image by u, v (computed only for an image leaf).
 // Texture value of an already resolved leaf whose marble value (if Perlin) is `pn`.
-__device__ __forceinline__ v3 leaf_texture_value(const DScene& S, int leaf, double pn, int prim, int face,
-                                                 const Hit& h) {
-  const DTex& tx = S.texs[leaf];
+__device__ __forceinline__ v3 leaf_texture_value(const DScene& S, const DTex* texs, int leaf, double pn, int prim,
+                                                 int face, const Hit& h) {
+  const DTex& tx = texs[leaf];
   if (tx.kind == RT_TEX_SOLID) return V(tx.color[0], tx.color[1], tx.color[2]);  // solid.rs:17-21
   if (tx.kind == RT_TEX_PERLIN) return V(pn, pn, pn);
   const UV uv = hit_uv(S.prims[prim], face, h);
@@ -2097,9 +2110,10 @@ template <bool DRAWN = false>
 __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int leaf, double pn, v3 r, v3 un,
                                           Rng& rng, uint64_t seed, v3& o, v3& d, const Hit& h, int prim,
                                           int face, v3& att, v3& em) {
+  const DTex* texs = S.texs;
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
     PH_COUNT(21);
-    v3 e = leaf_texture_value(S, leaf, pn, prim, face, h);
+    v3 e = leaf_texture_value(S, texs, leaf, pn, prim, face, h);
     em = em + hmul(att, e);
     return false;
   }
@@ -2135,14 +2149,14 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
     return true;
   }
   if (m.kind == RT_MAT_ISOTROPIC) {  // book-2 isotropic (extension): random_in_unit_sphere, albedo
-    att = hmul(att, leaf_texture_value(S, leaf, pn, prim, face, h));
+    att = hmul(att, leaf_texture_value(S, texs, leaf, pn, prim, face, h));
     o = h.point;
     d = r;
     return true;
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
   PH_COUNT(19);
-  v3 a = leaf_texture_value(S, leaf, pn, prim, face, h);
+  v3 a = leaf_texture_value(S, texs, leaf, pn, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
     double s = dot(h.normal, scale(d, -1.0));
     em = em + hmul(att, scale(a, s / len(d)));
@@ -2161,12 +2175,12 @@ __device__ __forceinline__ bool shade_pre(const DScene& S, const DMat& m, int le
 // attenuation factor goes to `mul` (att = att * mul; 1 for a dielectric, exact) and its emission to
 // `emit` with `has_emit` (em = em + att * emit, applied before the factor — the reference's order for
 // the fairy light).  Same arithmetic as shade_pre.
-__device__ __forceinline__ bool shade_factor(const DScene& S, const DMat& m, int leaf, double pn, v3 r, v3 un,
+__device__ __forceinline__ bool shade_factor(const DScene& S, const DTex* texs, const DMat& m, int leaf, double pn, v3 r, v3 un,
                                              Rng& rng, v3& o, v3& d, const Hit& h, int prim, int face, v3& mul,
                                              v3& emit, bool& has_emit) {
   if (m.kind == RT_MAT_DIFFUSE_LIGHT) {  // lighting.rs:21-29: emits, never scatters
     PH_COUNT(21);
-    emit = leaf_texture_value(S, leaf, pn, prim, face, h);
+    emit = leaf_texture_value(S, texs, leaf, pn, prim, face, h);
     has_emit = true;
     return false;
   }
@@ -2200,14 +2214,14 @@ __device__ __forceinline__ bool shade_factor(const DScene& S, const DMat& m, int
     return true;
   }
   if (m.kind == RT_MAT_ISOTROPIC) {  // book-2 isotropic (extension): random_in_unit_sphere, albedo
-    mul = leaf_texture_value(S, leaf, pn, prim, face, h);
+    mul = leaf_texture_value(S, texs, leaf, pn, prim, face, h);
     o = h.point;
     d = r;
     return true;
   }
   // RT_MAT_LAMBERTIAN (lambertian.rs:21-37) / RT_MAT_FAIRY_LIGHT (lighting.rs:42-66)
   PH_COUNT(19);
-  v3 a = leaf_texture_value(S, leaf, pn, prim, face, h);
+  v3 a = leaf_texture_value(S, texs, leaf, pn, prim, face, h);
   if (m.kind == RT_MAT_FAIRY_LIGHT) {
     double s = dot(h.normal, scale(d, -1.0));
     emit = scale(a, s / len(d));

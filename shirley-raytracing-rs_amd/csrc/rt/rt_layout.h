@@ -165,6 +165,8 @@ struct DScene {
   double time0, time1;     // camera shutter (set per render call)
   const double* shutter;   // device copy of {time0, time1}: moving spheres read it at the use site (an
                            // opaque pointer: held in SGPRs across the megakernel's loop the two doubles spill)
+  int32_t n_lds_mats;      // 0, or n_mats / n_texs when the scene-in-LDS block also keeps the materials and
+  int32_t n_lds_texs;      // textures in LDS (after the Perlin tables)
 };
 
 struct DCamera {

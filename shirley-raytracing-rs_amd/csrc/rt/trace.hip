@@ -68,10 +68,21 @@ void trace_kernel(KParams P) {
                                   : nullptr;
   unsigned char* stk_base = lds_raw + (size_t)P.scene.n_lds_nodes4 * sizeof(N4) +
                             (MODE == kSceneLds ? (size_t)P.scene.n_lds_prims * sizeof(DPrim) +
-                                                     (size_t)P.scene.n_lds_perlin * sizeof(DPerlin)
+                                                     (size_t)P.scene.n_lds_perlin * sizeof(DPerlin) +
+                                                     (size_t)P.scene.n_lds_mats * sizeof(DMat) +
+                                                     (size_t)P.scene.n_lds_texs * sizeof(DTex)
                                                : 0);
   unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;  // [stack_depth4][THREADS] packed entries
   stage_nodes4<MODE>(P.scene, lds_nodes, lds_prims);
+  // the material and texture tables: the block's LDS copies when the scene-in-LDS block holds them
+  // (S.n_lds_mats, after the Perlin tables), else global memory (generic pointers either way)
+  const DMat* mats = P.scene.mats;
+  const DTex* texs = P.scene.texs;
+  if (MODE == kSceneLds && P.scene.n_lds_mats > 0) {
+    mats = reinterpret_cast<const DMat*>(reinterpret_cast<const DPerlin*>(lds_prims + P.scene.n_lds_prims) +
+                                         P.scene.n_lds_perlin);
+    texs = reinterpret_cast<const DTex*>(mats + P.scene.n_lds_mats);
+  }
 
   const DCamera& C = P.cam;
   const DWork& W = P.work;
@@ -162,11 +173,11 @@ void trace_kernel(KParams P) {
         const DPrim pr = (MODE == kSceneLds) ? lds_prims[prim] : S.prims[prim];  // (LDS copy when resident)
         hit_record<false, EXT>(S, pr, face, o, d, t_best, rng, seed, h);
         mat = pr.material;
-        mk = S.mats[mat].kind;
+        mk = mats[mat].kind;
         need_r = mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_METAL || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_ISOTROPIC;
         if (mk == RT_MAT_LAMBERTIAN || mk == RT_MAT_FAIRY_LIGHT || mk == RT_MAT_DIFFUSE_LIGHT || mk == RT_MAT_ISOTROPIC) {
-          leaf = resolve_texture(S, S.mats[mat].tex, h.point);
-          const DTex& tx = S.texs[leaf];
+          leaf = resolve_texture_t(texs, mats[mat].tex, h.point);
+          const DTex& tx = texs[leaf];
           if (tx.kind == RT_TEX_PERLIN) {
             need_pn = true;
             ptab = tx.table;
@@ -318,8 +329,8 @@ void trace_kernel(KParams P) {
       bool alive, has_emit = false;
       v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
       if (hit) {
-        const DMat m = S.mats[mat];
-        alive = shade_factor(S, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
+        const DMat m = mats[mat];
+        alive = shade_factor(S, texs, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
       } else {
         PH_COUNT(20);
 #if RT_KSCENE
@@ -555,7 +566,9 @@ __global__ __launch_bounds__(kHitThreads) void hit4_kernel(DScene S, const doubl
   DPrim* lds_prims = reinterpret_cast<DPrim*>(lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4));
   unsigned char* stk_base = lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4) +
                             (MODE == kSceneLds ? (size_t)S.n_lds_prims * sizeof(DPrim) +
-                                                     (size_t)S.n_lds_perlin * sizeof(DPerlin)
+                                                     (size_t)S.n_lds_perlin * sizeof(DPerlin) +
+                                                     (size_t)S.n_lds_mats * sizeof(DMat) +
+                                                     (size_t)S.n_lds_texs * sizeof(DTex)
                                                : 0);
   unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;
   stage_nodes4<MODE>(S, lds_nodes, lds_prims);
@@ -614,7 +627,9 @@ __global__ __launch_bounds__(kHitThreads) void probe_kernel(DScene S, const doub
                                   : nullptr;
   unsigned char* stk_base = lds_raw + (size_t)S.n_lds_nodes4 * sizeof(N4) +
                             (MODE == kSceneLds ? (size_t)S.n_lds_prims * sizeof(DPrim) +
-                                                     (size_t)S.n_lds_perlin * sizeof(DPerlin)
+                                                     (size_t)S.n_lds_perlin * sizeof(DPerlin) +
+                                                     (size_t)S.n_lds_mats * sizeof(DMat) +
+                                                     (size_t)S.n_lds_texs * sizeof(DTex)
                                                : 0);
   unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;
   stage_nodes4<MODE>(S, lds_nodes, lds_prims);
@@ -683,7 +698,7 @@ __global__ __launch_bounds__(kHitThreads) void probe_kernel(DScene S, const doub
   v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
   if (hit) {
     const DMat m = S.mats[mat];
-    alive = shade_factor(S, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
+    alive = shade_factor(S, S.texs, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
     r.front_face = h.front_face ? 1 : 0;
     r.t = h.t;
     r.point[0] = h.point.x; r.point[1] = h.point.y; r.point[2] = h.point.z;
@@ -710,9 +725,10 @@ __global__ __launch_bounds__(kHitThreads) void probe_kernel(DScene S, const doub
 // megakernel block LDS: [n_lds_nodes4 x node4_bytes][n_lds_prims x DPrim][n_lds_perlin x DPerlin]
 // [stack_depth4 x threads packed entries]
 size_t trace_lds_bytes(int n_lds_nodes4, int node4_size, int n_lds_prims, int n_lds_perlin, int stack_depth4,
-                       int threads) {
+                       int threads, int n_lds_mats, int n_lds_texs) {
   return (size_t)n_lds_nodes4 * node4_size + (size_t)n_lds_prims * sizeof(DPrim) +
-         (size_t)n_lds_perlin * sizeof(DPerlin) + (size_t)stack_depth4 * threads * kStack4EntryBytes;
+         (size_t)n_lds_perlin * sizeof(DPerlin) + (size_t)n_lds_mats * sizeof(DMat) + (size_t)n_lds_texs * sizeof(DTex) +
+         (size_t)stack_depth4 * threads * kStack4EntryBytes;
 }
 size_t hit_lds_bytes(int n_lds_nodes, int stack_depth) { return lds_bytes(n_lds_nodes, stack_depth, kHitThreads); }
 
@@ -726,7 +742,8 @@ static int node_mode4(const DScene& S) {
 template <int THREADS, int MODE, bool EXT>
 static hipError_t occupancy_impl1(const DScene& S, int* blocks_per_cu) {
   // allow dynamic LDS beyond the 64 KiB default (gfx950 has 160 KiB per CU)
-  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(S.exts != nullptr), S.n_lds_prims, S.n_lds_perlin, S.stack_depth4, THREADS);
+  const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(S.exts != nullptr), S.n_lds_prims, S.n_lds_perlin, S.stack_depth4, THREADS,
+                                     S.n_lds_mats, S.n_lds_texs);
   hipError_t e = hipFuncSetAttribute((const void*)trace_kernel<THREADS, MODE, EXT>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (e != hipSuccess) return e;
@@ -777,7 +794,8 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
 }
 
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
-  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, node4_bytes(p.scene.exts != nullptr), p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads);
+  const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, node4_bytes(p.scene.exts != nullptr), p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads,
+                                     p.scene.n_lds_mats, p.scene.n_lds_texs);
   if (threads == kTraceThreadsWide) {
     if (p.scene.n_lds_prims > 0)
       launch_trace1<kTraceThreadsWide, kSceneLds>(p, blocks, lds, stream);
@@ -819,7 +837,8 @@ template <int MODE, bool EXT>
 static hipError_t launch_hit4_1(const DScene& S, const double* rays, int n, double t_min, double t_max, HitOut* o,
                                 int blocks, hipStream_t stream) {
   const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(EXT), MODE == kSceneLds ? S.n_lds_prims : 0,
-                                     MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads);
+                                     MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads,
+                                     MODE == kSceneLds ? S.n_lds_mats : 0, MODE == kSceneLds ? S.n_lds_texs : 0);
   hipError_t e = hipFuncSetAttribute((const void*)hit4_kernel<MODE, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
@@ -855,7 +874,8 @@ template <int MODE, bool EXT>
 static hipError_t launch_probe_1(const DScene& S, const double* rays, int n, uint64_t seed, uint32_t sample,
                                  uint32_t draw, ProbeOut* o, int blocks, hipStream_t stream) {
   const size_t lds = trace_lds_bytes(S.n_lds_nodes4, node4_bytes(EXT), MODE == kSceneLds ? S.n_lds_prims : 0,
-                                     MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads);
+                                     MODE == kSceneLds ? S.n_lds_perlin : 0, S.stack_depth4, kHitThreads,
+                                     MODE == kSceneLds ? S.n_lds_mats : 0, MODE == kSceneLds ? S.n_lds_texs : 0);
   hipError_t e = hipFuncSetAttribute((const void*)probe_kernel<MODE, EXT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
