@@ -1178,7 +1178,8 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     // RT_BOX_TWO_PASS bits: box_t2 in the reference-scene (1) / book-2 (2) instances, box_t1f in the
     // reference-scene (4) / book-2 (8) ones, else the six-face sequence
     constexpr bool kTwoPass = (RT_BOX_TWO_PASS & (EXT ? 2 : 1)) != 0;
-    constexpr bool kOneFull = (RT_BOX_TWO_PASS & (EXT ? 8 : 4)) != 0;
+    // (the scene-in-LDS instances only: compiled into the L1/L2 ones it cost gen_spheres 0.7 %)
+    constexpr bool kOneFull = (RT_BOX_TWO_PASS & (EXT ? 8 : 4)) != 0 && (EXT || MODE == kSceneLds);
     double tx;
     if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te, tx)) continue;  // a RectBox's bounding box is its p[0..5]
     RT_STAT(++ptests);
