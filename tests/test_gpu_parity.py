@@ -638,3 +638,23 @@ def test_final_scene_on_the_narrow_block(gpu, monkeypatch):
     assert np.array_equal(narrow, wide)
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
     check_parity(narrow, ora, spp, frac_exact=exact_floor("final"))
+
+
+@pytest.mark.parametrize("name,width,aspect", [("random", 48, "std16x9"), ("cornell", 40, "square"),
+                                               ("earth", 48, "square"), ("final:6:60", 40, "square")])
+def test_lds_material_tables_change_nothing(gpu, monkeypatch, name, width, aspect):
+    """The scene-in-LDS block keeps the material and texture tables in LDS after the Perlin tables (rt_api.cpp
+    n_lds_mats): the frame is the one the global-memory tables give (SHIRLEY_NO_LDS_MATS, read
+    at upload), bit for bit."""
+    spp = 4
+    scene = rt.SceneBuilder.builtin(name, SEED).finalize(SEED)
+    cam = rt.scene_camera(name, width, aspect)
+    s = rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp)
+    gpu.upload(scene)
+    lds = gpu.render(cam, s)
+    monkeypatch.setenv("SHIRLEY_NO_LDS_MATS", "1")
+    gpu.upload(scene)
+    glob = gpu.render(cam, s)
+    monkeypatch.delenv("SHIRLEY_NO_LDS_MATS")
+    gpu.upload(scene)
+    assert np.array_equal(lds, glob)
