@@ -1337,28 +1337,24 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   c->mk_threads = wide ? wide_threads : kTraceThreads;
   S.n_lds_nodes = lds_nodes_for(kHitThreads * 8LL * S.stack_depth);
   S.n_lds_nodes4 = wide ? (int32_t)nodes4.size() : lds_count(stack4_bytes, n4_bytes, nodes4.size());
-  // primitives too, when they fit beside the wide block's tree and stacks (leaf tests from LDS)
-  const bool prims_lds = wide && wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) <= kLdsBytes &&
-                         !getenv("SHIRLEY_NO_LDS_PRIMS");
+  // primitives too, with the material and texture tables (the megakernel's scene-in-LDS instance reads all
+  // three from LDS), when they fit beside the wide block's tree and stacks
+  const long long mt_bytes = (long long)mats.size() * (long long)sizeof(DMat) + (long long)texs.size() * (long long)sizeof(DTex);
+  const bool prims_lds = wide && wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) + mt_bytes <= kLdsBytes &&
+                         !getenv("SHIRLEY_NO_LDS_PRIMS") && !getenv("SHIRLEY_NO_LDS_MATS");
   S.n_lds_prims = prims_lds ? d->n_objects : 0;
   // and the Perlin tables (marble's ~210 gathers per evaluation from LDS)
   const bool perlin_lds = prims_lds && d->n_perlin > 0 &&
-                          wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) +
+                          wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) + mt_bytes +
                                   (long long)d->n_perlin * (long long)sizeof(DPerlin) <= kLdsBytes &&
                           !getenv("SHIRLEY_NO_LDS_PERLIN");
   S.n_lds_perlin = perlin_lds ? d->n_perlin : 0;
-  // and the material and texture tables (the record / shading reads: headline +1.0 %, Cornell +0.7 %,
-  // DESIGN.md §5; SHIRLEY_NO_LDS_MATS: tuning switch).  The wavefront and split engines keep their own
-  // LDS layouts and read them from global memory (their scene copies carry n_lds_mats = 0).
-  S.n_lds_mats = S.n_lds_texs = 0;
-  if (prims_lds && (d->n_perlin == 0 || perlin_lds) && !getenv("SHIRLEY_NO_LDS_MATS") &&
-      wide_bytes + (long long)d->n_objects * (long long)sizeof(DPrim) +
-              (long long)S.n_lds_perlin * (long long)sizeof(DPerlin) +
-              (long long)mats.size() * (long long)sizeof(DMat) + (long long)texs.size() * (long long)sizeof(DTex) <=
-          kLdsBytes) {
-    S.n_lds_mats = (int32_t)mats.size();
-    S.n_lds_texs = (int32_t)texs.size();
-  }
+  // the material and texture tables ride with the primitives (the record / shading reads: headline +1.0 %,
+  // Cornell +0.7 %; SHIRLEY_NO_LDS_MATS keeps all three in global memory).  The wavefront and
+  // split engines keep their own LDS layouts and read them from global memory (their scene copies carry
+  // n_lds_mats = 0).
+  S.n_lds_mats = prims_lds ? (int32_t)mats.size() : 0;
+  S.n_lds_texs = prims_lds ? (int32_t)texs.size() : 0;
 
   int bpc = 0;
   HIP_TRY(c, trace_occupancy(S, c->mk_threads, &bpc));

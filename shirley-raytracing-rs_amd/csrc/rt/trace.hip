@@ -74,11 +74,13 @@ void trace_kernel(KParams P) {
                                                : 0);
   unsigned* stk = reinterpret_cast<unsigned*>(stk_base) + tid;  // [stack_depth4][THREADS] packed entries
   stage_nodes4<MODE>(P.scene, lds_nodes, lds_prims);
-  // the material and texture tables: the block's LDS copies when the scene-in-LDS block holds them
-  // (S.n_lds_mats, after the Perlin tables), else global memory (generic pointers either way)
+  // the material and texture tables: the scene-in-LDS block's copies (after the Perlin tables: the host
+  // places the primitives in LDS only together with them), else global memory.  Unconditional per
+  // instance, so the compiler reads the LDS copies with ds_read (a runtime choice made every read a FLAT
+  // load).
   const DMat* mats = P.scene.mats;
   const DTex* texs = P.scene.texs;
-  if (MODE == kSceneLds && P.scene.n_lds_mats > 0) {
+  if constexpr (MODE == kSceneLds) {
     mats = reinterpret_cast<const DMat*>(reinterpret_cast<const DPerlin*>(lds_prims + P.scene.n_lds_prims) +
                                          P.scene.n_lds_perlin);
     texs = reinterpret_cast<const DTex*>(mats + P.scene.n_lds_mats);
