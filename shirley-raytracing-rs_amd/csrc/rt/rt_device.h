@@ -1152,7 +1152,14 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     if (!sphere_t_sure(pr.p, o, d, ra, ra_ok, t_min, t_best, t, sure)) continue;
     if (!sure) {
       const DPrim* pp = &pr;
-      asm volatile("" : "+v"(pp));
+      if constexpr (MODE == kSceneLds) {  // (laundered as an LDS pointer, so the re-read stays a ds_read)
+        typedef __attribute__((address_space(3))) const DPrim LdsPrim;
+        LdsPrim* lp = (LdsPrim*)pp;
+        asm volatile("" : "+v"(lp));
+        pp = (const DPrim*)lp;
+      } else {
+        asm volatile("" : "+v"(pp));
+      }
       if (!slab_sphere(pp->p, o, inv, ns, t_min, t_best)) continue;
     }
     t_best = t; best = leaf; face_best = -1; hit = true;
@@ -1932,7 +1939,9 @@ __device__ __forceinline__ v3 image_texel(const DTex& tx, double u, double v) {
   double vv = 1.0 - ((v > 0.0) ? ((v < 1.0) ? v : 1.0) : 0.0);
   uint32_t ix = (uint32_t)(uu * (double)(im.width - 1));
   uint32_t iy = (uint32_t)(vv * (double)(im.height - 1));
-  const uint8_t* px = im.texels + ((size_t)iy * (size_t)im.width + ix) * 3;
+  // (the texels are in global memory: typed so, a texture record read from LDS does not make them FLAT loads)
+  typedef __attribute__((address_space(1))) const uint8_t GTexel;
+  GTexel* px = (GTexel*)im.texels + ((size_t)iy * (size_t)im.width + ix) * 3;
   const double cs = 1.0 / 255.0;
   return V((double)px[0] * cs, (double)px[1] * cs, (double)px[2] * cs);
 }
