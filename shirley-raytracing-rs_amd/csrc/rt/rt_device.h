@@ -212,7 +212,8 @@ __device__ __forceinline__ v3 random_in_unit_disk(Rng& r, uint64_t seed) {
 // One draw of a side stream (book-2 extensions): Philox4x32-10 at counter
 // (c0, sample, pixel, stream) with stream >= 2^30 — disjoint from the path streams (word 3 = 0) and
 // the scene streams (word 2 = 0xFFFFFFFF, small stream ids), so side draws never shift the
-// reference-order draws of a path.  Without philox10's SGPR pinning (the key may live in VGPRs here).
+// reference-order draws of a path.  The seed is the launch's (uniform), so the round keys are pinned to
+// SGPRs as in philox10: hoisted, they were 18 of the book-2 instances' spilled SGPRs.
 constexpr uint32_t kStreamTime = 0x40000000u;    // the ray time of (pixel, sample)
 constexpr uint32_t kStreamMedium = 0x80000000u;  // | prim: a medium's free-flight draw, c0 = path draw index
 __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t sample, uint32_t pixel,
@@ -224,6 +225,7 @@ __device__ __forceinline__ double side_draw(uint64_t seed, uint32_t c0, uint32_t
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
+    asm volatile("" : "+s"(k0), "+s"(k1));
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     const uint32_t n0 = xor3((uint32_t)(p1 >> 32), c1, k0), n2 = xor3((uint32_t)(p0 >> 32), c3, k1);
     c0 = n0;
