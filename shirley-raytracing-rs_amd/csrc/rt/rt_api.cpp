@@ -578,12 +578,13 @@ struct Collapse4 {
   }
 };
 
+// use_dp: the optimal collapse (Collapse4) instead of the greedy one (open the largest-area internal
+// child until four slots are filled).  rt_scene_upload picks it for the scenes the megakernel runs with
+// the whole scene in LDS, greedy for the rest.
 void flatten4(const BuiltTree& t, const rt_scene_desc* d, double delta, std::vector<DNode4F>& out,
-              int32_t& stack_bound) {
-  // greedy by default: the optimal collapse tests ~3 % fewer boxes per segment on random_scene but
-  // measured no faster (the wave's slowest lane, not the mean, sets a step's cost)
+              int32_t& stack_bound, bool use_dp) {
   Collapse4 dp;
-  if (t.root >= 0 && getenv("SHIRLEY_COLLAPSE_DP")) dp.build(t);  // tuning switch
+  if (t.root >= 0 && use_dp) dp.build(t);
   out.clear();
   DNode4F top{};
   for (int k = 0; k < 4; ++k) {
@@ -1150,7 +1151,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   std::vector<DNode4F> nodes4;
   int32_t stack4 = 1;
   const Inflation infl = inflation_for(tree);
-  flatten4(tree, d, infl.delta, nodes4, stack4);
+  flatten4(tree, d, infl.delta, nodes4, stack4, false);
   std::vector<DPrim> prims(std::max(1, d->n_objects));
   std::vector<DExt> exts;
   for (int i = 0; i < d->n_objects; ++i) {
@@ -1247,6 +1248,30 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   }
   if (texels.empty()) texels.resize(16);
 
+  // The 4-wide collapse: the optimal one (fewest expected node visits by area) for a reference scene that
+  // will run in the scene-in-LDS instance — Cornell +15 %, headline +0.3 % — and the greedy one for the
+  // scenes read through L1/L2 (gen_spheres −1.4 %, final_scene −1.6 % with the optimal one).
+  // The same test as the placement below (tree, stacks, primitives and tables within the wide block's
+  // LDS), on either tree.  SHIRLEY_COLLAPSE_DP=1 / =0: always / never (tuning).
+  {
+    const size_t mt = mats.size() * sizeof(DMat) + texs.size() * sizeof(DTex);
+    auto scene_in_lds = [&](const std::vector<DNode4F>& n4, int32_t s4) {
+      return (long long)s4 * kTraceThreadsWide * kStack4EntryBytes + (long long)n4.size() * (long long)sizeof(DNode4F) +
+                 (long long)d->n_objects * (long long)sizeof(DPrim) + (long long)mt <=
+             kLdsBytes;
+    };
+    const char* e = getenv("SHIRLEY_COLLAPSE_DP");
+    const bool want = e ? atoi(e) != 0 : (exts.empty() && placement == 0 && scene_in_lds(nodes4, stack4));
+    if (want) {
+      std::vector<DNode4F> dp4;
+      int32_t dp_stack = 1;
+      flatten4(tree, d, infl.delta, dp4, dp_stack, true);
+      if (e || scene_in_lds(dp4, dp_stack)) {
+        nodes4.swap(dp4);
+        stack4 = dp_stack;
+      }
+    }
+  }
   if ((st = upload(c, c->nodes, nodes.data(), nodes.size() * sizeof(DNode)))) return st;
   // book-2 scenes run the EXT kernel instances, which read the compact node layout (rt_layout.h)
   const int n4_bytes = node4_bytes(!exts.empty());

@@ -658,3 +658,30 @@ def test_lds_material_tables_change_nothing(gpu, monkeypatch, name, width, aspec
     monkeypatch.delenv("SHIRLEY_NO_LDS_MATS")
     gpu.upload(scene)
     assert np.array_equal(lds, glob)
+
+
+@pytest.mark.parametrize("name,width,aspect", [("random", 48, "std16x9"), ("cornell", 40, "square"),
+                                               ("box-light", 48, "std16x9"), ("spheres", 48, "std16x9")])
+def test_collapse_choice_changes_nothing(gpu, monkeypatch, name, width, aspect):
+    """The 4-wide collapse is picked per scene at upload (rt_api.cpp rt_scene_upload: the optimal collapse for
+    scene-in-LDS reference scenes, greedy otherwise).  The tree only orders and culls the
+    node tests — every leaf test stays exact — so the optimal, the greedy and the automatic choice give the
+    same frame, bit for bit, and that frame is the oracle's within the parity gate."""
+    spp = 4
+    scene = rt.SceneBuilder.builtin(name, SEED).finalize(SEED)
+    cam = rt.scene_camera(name, width, aspect)
+    s = rt.RenderSettings(samples=spp, seed=SEED, sample_chunk=spp)
+    frames = {}
+    for mode in ("auto", "0", "1"):
+        if mode == "auto":
+            monkeypatch.delenv("SHIRLEY_COLLAPSE_DP", raising=False)
+        else:
+            monkeypatch.setenv("SHIRLEY_COLLAPSE_DP", mode)
+        gpu.upload(scene)
+        frames[mode] = gpu.render(cam, s)
+    monkeypatch.delenv("SHIRLEY_COLLAPSE_DP", raising=False)
+    gpu.upload(scene)
+    assert np.array_equal(frames["auto"], frames["0"])
+    assert np.array_equal(frames["auto"], frames["1"])
+    ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
+    check_parity(frames["auto"], ora, spp, frac_exact=PARITY_EXACT)
