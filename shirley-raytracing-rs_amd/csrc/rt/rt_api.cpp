@@ -1261,7 +1261,8 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
              kLdsBytes;
     };
     const char* e = getenv("SHIRLEY_COLLAPSE_DP");
-    const bool want = e ? atoi(e) != 0 : (exts.empty() && placement == 0 && scene_in_lds(nodes4, stack4));
+    const bool want = e ? atoi(e) != 0
+                        : (exts.empty() && (placement == 0 || placement == RT_BVH_NODES_LDS) && scene_in_lds(nodes4, stack4));
     if (want) {
       std::vector<DNode4F> dp4;
       int32_t dp_stack = 1;
