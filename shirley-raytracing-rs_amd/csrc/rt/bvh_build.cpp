@@ -147,8 +147,10 @@ struct SahBuilder {
   std::vector<std::array<double, 3>> cen;
 
   bool sweep = false;  // exact SAH over every object boundary instead of 32 centroid bins
+  const std::vector<double>* weight = nullptr;  // per-object test cost (sweep only; null: 1 each)
   std::vector<int> tmp;
-  std::vector<double> right_sa;
+  std::vector<double> right_sa, right_w;
+  double w(int x) const { return weight ? (*weight)[x] : 1.0; }
 
   explicit SahBuilder(const std::vector<Box>& b) : boxes(b) {}
 
@@ -171,19 +173,25 @@ struct SahBuilder {
     double best_cost = INFINITY;
     int best_axis = -1, best_i = -1;
     right_sa.resize(n);
+    right_w.resize(n);
     for (int a = 0; a < 3; ++a) {
       tmp.assign(items.begin() + begin, items.begin() + end);
       std::sort(tmp.begin(), tmp.end(), [&](int x, int y) { return before(x, y, a); });
       Box acc = boxes[tmp[n - 1]];
+      double wr = 0.0;
       for (int i = n - 1; i >= 1; --i) {  // right_sa[i]: objects [i, n)
         if (i < n - 1) acc = surrounding(acc, boxes[tmp[i]]);
         right_sa[i] = surface(acc);
+        wr += w(tmp[i]);
+        right_w[i] = wr;
       }
       acc = boxes[tmp[0]];
+      double wl = 0.0;
       for (int i = 1; i < n; ++i) {  // split before object i: left [0, i), right [i, n)
         if (i > 1) acc = surrounding(acc, boxes[tmp[i - 1]]);
+        wl += w(tmp[i - 1]);
         if (ckey(tmp[i - 1], a) == ckey(tmp[i], a)) continue;  // not a separating plane
-        const double cost = surface(acc) * i + right_sa[i] * (n - i);
+        const double cost = weight ? surface(acc) * wl + right_sa[i] * right_w[i] : surface(acc) * i + right_sa[i] * (n - i);
         if (cost < best_cost) { best_cost = cost; best_axis = a; best_i = i; }
       }
     }
@@ -306,10 +314,11 @@ BuiltTree build_reference_tree(const std::vector<Box>& boxes) {
   return out;
 }
 
-BuiltTree build_sah_tree(const std::vector<Box>& boxes, bool sweep) {
+BuiltTree build_sah_tree(const std::vector<Box>& boxes, bool sweep, const std::vector<double>* weight) {
   BuiltTree out;
   SahBuilder b(boxes);
   b.sweep = sweep;
+  b.weight = weight;
   for (int i = 0; i < (int)boxes.size(); ++i) {
     const Box& x = boxes[i];
     bool never = false;

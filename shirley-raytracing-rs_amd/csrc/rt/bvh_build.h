@@ -35,7 +35,8 @@ BuiltTree build_reference_tree(const std::vector<Box>& boxes);
 // false: 32 centroid bins.  Objects whose box can never pass the slab test (min > max on an axis:
 // the reference's negative-radius spheres, sphere.rs:54-60) are left out; every other object keeps
 // its own box as its leaf box.
-BuiltTree build_sah_tree(const std::vector<Box>& boxes, bool sweep = false);
+// weight (sweep only): per-object test cost in the split cost, sum over a side instead of its count.
+BuiltTree build_sah_tree(const std::vector<Box>& boxes, bool sweep = false, const std::vector<double>* weight = nullptr);
 
 // Max number of branch nodes on a root-to-leaf path.
 int32_t tree_branch_depth(const BuiltTree& t);
