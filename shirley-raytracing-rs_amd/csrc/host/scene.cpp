@@ -363,18 +363,6 @@ void perlin_generate(uint64_t seed, uint32_t table_index, rt_perlin_table* out) 
   }
 }
 
-std::string earth_texture_path() {
-  if (const char* env = std::getenv("SHIRLEY_ASSETS")) return std::string(env) + "/earthmap.rgb8.gz";
-  Dl_info info;
-  if (dladdr((void*)&earth_texture_path, &info) && info.dli_fname) {
-    std::string so = info.dli_fname;
-    size_t slash = so.rfind('/');
-    std::string dir = (slash == std::string::npos) ? "." : so.substr(0, slash);
-    return dir + "/../assets/earthmap.rgb8.gz";
-  }
-  return "assets/earthmap.rgb8.gz";
-}
-
 static bool read_file(const std::string& path, std::string* out) {
   std::ifstream f(path, std::ios::binary);
   if (!f) return false;
@@ -384,26 +372,51 @@ static bool read_file(const std::string& path, std::string* out) {
   return true;
 }
 
-static bool load_rgb8_gz(const std::string& path, int32_t* w, int32_t* h, std::vector<uint8_t>* rgb, std::string* err) {
-  gzFile f = gzopen(path.c_str(), "rb");
-  if (!f) { *err = "cannot open " + path; return false; }
+// "RGB8 <w> <h>\n" + w*h*3 bytes, gzip-wrapped (tools/decode_earthmap.py)
+static bool parse_rgb8_gz(const unsigned char* gz, size_t gz_len, const std::string& what, int32_t* w, int32_t* h,
+                          std::vector<uint8_t>* rgb, std::string* err) {
+  z_stream zs{};
+  if (inflateInit2(&zs, 16 + MAX_WBITS) != Z_OK) { *err = "inflateInit failed for " + what; return false; }
+  zs.next_in = const_cast<Bytef*>(gz);
+  zs.avail_in = (uInt)gz_len;
   std::string data;
-  char buf[1 << 16];
-  int n;
-  while ((n = gzread(f, buf, sizeof buf)) > 0) data.append(buf, (size_t)n);
-  gzclose(f);
+  unsigned char buf[1 << 16];
+  int zr;
+  do {
+    zs.next_out = buf;
+    zs.avail_out = sizeof buf;
+    zr = inflate(&zs, Z_NO_FLUSH);
+    data.append((const char*)buf, sizeof buf - zs.avail_out);
+  } while (zr == Z_OK);
+  inflateEnd(&zs);
+  if (zr != Z_STREAM_END) { *err = "corrupt gzip stream in " + what; return false; }
   size_t nl = data.find('\n');
   int ww = 0, hh = 0;
   if (nl == std::string::npos || std::sscanf(data.c_str(), "RGB8 %d %d", &ww, &hh) != 2 || ww < 1 || hh < 1) {
-    *err = "bad RGB8 header in " + path;
+    *err = "bad RGB8 header in " + what;
     return false;
   }
   size_t need = (size_t)ww * hh * 3;
-  if (data.size() - nl - 1 != need) { *err = "truncated RGB8 data in " + path; return false; }
+  if (data.size() - nl - 1 != need) { *err = "truncated RGB8 data in " + what; return false; }
   rgb->assign(data.begin() + (long)nl + 1, data.end());
   *w = ww;
   *h = hh;
   return true;
+}
+
+static bool load_rgb8_gz(const std::string& path, int32_t* w, int32_t* h, std::vector<uint8_t>* rgb, std::string* err) {
+  std::string gz;
+  if (!read_file(path, &gz)) { *err = "cannot open " + path; return false; }
+  return parse_rgb8_gz((const unsigned char*)gz.data(), gz.size(), path, w, h, rgb, err);
+}
+
+// linked in by earth_embed.S (the reference's include_bytes!, image_texture.rs:11,18-20)
+extern "C" const unsigned char shirley_earth_rgb8_gz[];
+extern "C" const unsigned char shirley_earth_rgb8_gz_end[];
+
+bool load_earth_builtin(int32_t* w, int32_t* h, std::vector<uint8_t>* rgb, std::string* err) {
+  return parse_rgb8_gz(shirley_earth_rgb8_gz, (size_t)(shirley_earth_rgb8_gz_end - shirley_earth_rgb8_gz),
+                       "EarthBuiltin (embedded)", w, h, rgb, err);
 }
 
 static uint32_t be32(const unsigned char* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
@@ -498,13 +511,15 @@ struct Loader {
   uint64_t seed;
   std::map<std::string, int32_t> image_cache;  // identical files share texels (no semantic change)
 
+  // path "" = EarthBuiltin (embedded texels), anything else a user file (ImagePath)
   int32_t image(const std::string& path) {
     auto it = image_cache.find(path);
     if (it != image_cache.end()) return it->second;
     int32_t w = 0, h = 0;
     std::vector<uint8_t> px;
     std::string err;
-    if (!load_image_file(path, &w, &h, &px, &err)) throw std::runtime_error(err);
+    bool ok = path.empty() ? load_earth_builtin(&w, &h, &px, &err) : load_image_file(path, &w, &h, &px, &err);
+    if (!ok) throw std::runtime_error(err);
     d.image_pixels.push_back(std::move(px));
     rt_image im{w, h, nullptr};
     d.images.push_back(im);
@@ -533,7 +548,7 @@ struct Loader {
       }
       case TextureLoader::EarthBuiltin:
         x.kind = RT_TEX_IMAGE;
-        x.table = image(earth_texture_path());
+        x.table = image("");
         break;
       case TextureLoader::ImagePath:
         x.kind = RT_TEX_IMAGE;

@@ -117,8 +117,9 @@ struct SceneBuilder {
 // Perlin::new from a seeded stream (perlin/mod.rs:73-85, 126-139)
 void perlin_generate(uint64_t seed, uint32_t table_index, rt_perlin_table* out);
 
-// decoded image textures (image_texture.rs:11-31); EarthBuiltin = assets/earthmap.rgb8.gz
+// decoded image textures (image_texture.rs:11-31): ImagePath files (PNG / .rgb8.gz)
 bool load_image_file(const std::string& path, int32_t* w, int32_t* h, std::vector<uint8_t>* rgb, std::string* err);
-std::string earth_texture_path();
+// EarthBuiltin: assets/earthmap.rgb8.gz linked into the library (earth_embed.S), like include_bytes!
+bool load_earth_builtin(int32_t* w, int32_t* h, std::vector<uint8_t>* rgb, std::string* err);
 
 }  // namespace host

@@ -7,6 +7,7 @@ import math
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -212,6 +213,44 @@ def test_earth_texture_loads():
     a = np.ctypeslib.as_array(p, shape=(512 * 1024 * 3,)).copy()
     N.host_lib().sh_free(p)
     assert 85 < a.mean() < 95
+
+
+EARTH_CHILD = r"""
+import ctypes as C, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from raytracer import _native as N
+s = C.c_void_p()
+N.host_check(N.host_lib().sh_scene_builtin(b"earth", 0x5EED, C.byref(s)))
+d = C.c_void_p()
+N.host_check(N.host_lib().sh_scene_finalize(s, 0x5EED, C.byref(d)))
+v = N.host_lib().sh_desc_view(d).contents
+assert v.n_images == 1, v.n_images
+im = v.images[0]
+px = np.ctypeslib.as_array(im.rgb, shape=(im.height * im.width * 3,))
+print(im.width, im.height, int(px.astype(np.int64).sum()), N.host_lib()._name)
+"""
+
+
+@pytest.mark.parametrize("lib_dir", ["lib", "lib/diag"])
+def test_earth_builtin_needs_no_asset_lookup(lib_dir, tmp_path):
+    """EarthBuiltin is linked into the library (earth_embed.S, the reference's include_bytes!,
+    image_texture.rs:11,18-20): every copy of libshirley_host.so finalises the earth scene with
+    SHIRLEY_ASSETS unset, from any working directory, and the texels equal the committed asset."""
+    pkg = os.path.join(REPO, "shirley-raytracing-rs_amd")
+    env = {k: v for k, v in os.environ.items() if k not in ("SHIRLEY_ASSETS",)}
+    env["SHIRLEY_LIB_DIR"] = os.path.join(pkg, lib_dir)
+    env["SHIRLEY_NO_TORCH"] = "1"
+    r = subprocess.run([sys.executable, "-c", EARTH_CHILD, pkg], env=env, cwd=str(tmp_path),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    w, h, total, name = r.stdout.split()
+    assert name.startswith(env["SHIRLEY_LIB_DIR"])
+    import gzip
+    blob = gzip.open(os.path.join(pkg, "assets", "earthmap.rgb8.gz")).read()
+    texels = np.frombuffer(blob[blob.index(b"\n") + 1:], dtype=np.uint8)
+    assert (int(w), int(h)) == (1024, 512)
+    assert int(total) == int(texels.astype(np.int64).sum())
 
 
 def test_tonemap_equals_oracle():

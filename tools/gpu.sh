@@ -27,7 +27,7 @@
 #   gpurun -- 'bash tools/gpu.sh r03b "ab:main||;f32s||;main||;f32s||"'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-export SHIRLEY_ASSETS=${SHIRLEY_ASSETS:-$PWD/shirley-raytracing-rs_amd/assets}  # exp/<variant> libs resolve assets here
+
 tag=$1; shift
 out=gpurun_out/$tag
 mkdir -p "$out"

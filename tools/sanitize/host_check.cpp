@@ -171,7 +171,7 @@ int main(int argc, char** argv) {
     std::fprintf(stderr, "usage: %s <asset_dir> <n_mutants> [seed]\n", argv[0]);
     return 2;
   }
-  setenv("SHIRLEY_ASSETS", argv[1], 1);
+  (void)argv[1];  // asset dir: unused since EarthBuiltin is linked in (earth_embed.S)
   const long n_mut = std::atol(argv[2]);
   XorShift rng{argc > 3 ? std::strtoull(argv[3], nullptr, 0) : 0x5EEDull};
 
