@@ -657,14 +657,27 @@ static void* dupmem(const void* p, size_t n) {
   return q;
 }
 
+/* Does texture ti read the hit's u, v?  Only an image leaf does (image_texture.rs:34-56). */
+static int texture_uses_uv(const rt_scene_desc* d, int32_t ti) {
+  if (ti < 0 || ti >= d->n_textures) return 0;
+  const rt_texture* t = &d->textures[ti];
+  if (t->kind == RT_TEX_IMAGE) return 1;
+  if (t->kind == RT_TEX_CHECKER) return texture_uses_uv(d, t->odd) || texture_uses_uv(d, t->even);
+  return 0;
+}
 /* Book-2 (extension): Translate(RotateY(sphere)) of a plain sphere is the sphere about the moved
  * centre, so such an instance is flattened into a world-space sphere before anything else reads it —
  * centre (cs cx + sn cz + off.x, cy + off.y, -sn cx + cs cz + off.z), the same formula that maps an
  * instance's hit point back to the world (ext_object_hit) — and takes the reference sphere path.  The
- * host (rt_api.cpp flat_object) flattens identically.  Exact in real arithmetic; the records differ
- * from per-ray instancing at the last bit. */
-static void flatten_instanced_sphere(rt_object* o) {
+ * host (rt_api.cpp flat_object) flattens by the same rule.  t, point and normal agree with per-ray
+ * instancing in real arithmetic (the records differ at the last bit); u, v do not under a
+ * rotation, so a rotated sphere is flattened only when its material never reads them, and keeps its
+ * angle (transform = 0) for the hit query's u, v (or_scene_hit_at). */
+static void flatten_instanced_sphere(const rt_scene_desc* d, rt_object* o) {
   if (o->geometry != RT_GEOM_SPHERE || !o->transform || o->medium) return;
+  if (o->rotate_y_deg != 0.0 &&
+      (o->material < 0 || o->material >= d->n_materials || texture_uses_uv(d, d->materials[o->material].texture)))
+    return;
   double cs, sn;
   rotate_y_cs(o, &cs, &sn);
   const double cx = o->p[0], cy = o->p[1], cz = o->p[2];
@@ -672,7 +685,6 @@ static void flatten_instanced_sphere(rt_object* o) {
   o->p[1] = cy + o->offset[1];
   o->p[2] = (-sn * cx + cs * cz) + o->offset[2];
   o->transform = 0;
-  o->rotate_y_deg = 0.0;
   o->offset[0] = o->offset[1] = o->offset[2] = 0.0;
 }
 
@@ -681,7 +693,7 @@ or_scene* or_scene_new(const rt_scene_desc* d) {
   or_scene* s = (or_scene*)calloc(1, sizeof(or_scene));
   s->desc = *d;
   s->objects = (rt_object*)dupmem(d->objects, sizeof(rt_object) * (size_t)d->n_objects);
-  for (int32_t i = 0; i < d->n_objects; ++i) flatten_instanced_sphere(&s->objects[i]);
+  for (int32_t i = 0; i < d->n_objects; ++i) flatten_instanced_sphere(d, &s->objects[i]);
   s->desc.objects = s->objects;
   s->materials = (rt_material*)dupmem(d->materials, sizeof(rt_material) * (size_t)d->n_materials);
   s->textures = (rt_texture*)dupmem(d->textures, sizeof(rt_texture) * (size_t)d->n_textures);
@@ -1194,7 +1206,19 @@ void or_scene_hit_at(const or_scene* s, const double ray[6], double t_min, doubl
   int32_t obj = -1;
   memset(out, 0, sizeof(*out));
   out->object = -1;
-  if (scene_hit(s, &w, &r, t_min, t_max, &h, &obj)) hit_out(&h, obj, out);
+  if (scene_hit(s, &w, &r, t_min, t_max, &h, &obj)) {
+    const rt_object* o = &s->objects[obj];
+    if (o->geometry == RT_GEOM_SPHERE && !o->transform && o->rotate_y_deg != 0.0) {
+      /* a flattened rotated instance: u, v on its object-frame outward normal (sphere.rs:17-26) */
+      double cs, sn;
+      rotate_y_cs(o, &cs, &sn);
+      v3 n = h.front_face ? h.normal : vscale(h.normal, -1.0);
+      v3 on = V(cs * n.x - sn * n.z, n.y, sn * n.x + cs * n.z);
+      h.u = (OR_ATAN2(-on.z, on.x) + PI_) / (2.0 * PI_);
+      h.v = OR_ACOS(-on.y) / PI_;
+    }
+    hit_out(&h, obj, out);
+  }
   free(w.stack);
 }
 void or_scene_hit(const or_scene* s, const double ray[6], double t_min, double t_max, or_hit* out) {

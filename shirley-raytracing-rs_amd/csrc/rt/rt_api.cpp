@@ -117,6 +117,8 @@ struct rt_ctx {
   std::vector<hipEvent_t> pass_ev;   // before / after the trace launch of each sample pass
   std::vector<KBlock> host_blocks;    // host sources of the device KBlocks (KParams.kconst)
   uint64_t digest = 0;               // rt_scene_digest of the uploaded scene
+  // flattened rotated spheres (flat_object): object index -> RotateY's cos, sin, for rt_scene_hit's u, v
+  std::vector<std::pair<int32_t, std::pair<double, double>>> uv_fixups;
   uint64_t host_samples = 0;  // samples of a frame served without a trace kernel (max_depth == 0)
   double lap_ms[3] = {0, 0, 0};
   // multi-GPU: this rank's packed tiles, the root's gathered buffer, and (root of rt_render_multi)
@@ -183,13 +185,31 @@ void rotate_y_cs(const rt_object& o, double& cs, double& sn) {
   cs = std::cos(rad);
   sn = std::sin(rad);
 }
+// Does texture `ti` (a tree: children are earlier textures, validate()) read the hit's u, v?  Only an
+// image leaf does (image_texture.rs:34-56); checker and marble read the point, solid nothing.
+bool texture_uses_uv(const rt_scene_desc* d, int32_t ti) {
+  if (ti < 0 || ti >= d->n_textures) return false;
+  const rt_texture& t = d->textures[ti];
+  if (t.kind == RT_TEX_IMAGE) return true;
+  if (t.kind == RT_TEX_CHECKER) return texture_uses_uv(d, t.odd) || texture_uses_uv(d, t.even);
+  return false;
+}
 // Book-2: Translate(RotateY(sphere)) of a plain sphere is the sphere about the moved centre — flattened
 // into a world-space sphere before the tree is built, by the formula that maps an instance's hit point
 // back to the world, so the instances take the reference sphere path (sphere leaf loop, no per-leaf ray
-// transform).  The oracle flattens identically (oracle.c flatten_instanced_sphere).  DESIGN.md §10.
-rt_object flat_object(const rt_object& o) {
+// transform).  t, point and normal agree with per-ray instancing in real arithmetic; u, v do not under a
+// rotation (the instance's u is taken in its own frame, shifted by angle / 360), so a rotated sphere is
+// flattened only when its material never reads u, v; rt_scene_hit then derives the instance's u, v from
+// the record (uv_fixups).  The oracle flattens by the same rule (oracle.c flatten_instanced_sphere).
+// DESIGN.md §10.
+bool flattens(const rt_scene_desc* d, const rt_object& o) {
+  if (o.geometry != RT_GEOM_SPHERE || !o.transform || o.medium) return false;
+  if (o.rotate_y_deg == 0.0) return true;
+  return o.material >= 0 && o.material < d->n_materials && !texture_uses_uv(d, d->materials[o.material].texture);
+}
+rt_object flat_object(const rt_scene_desc* d, const rt_object& o) {
   rt_object f = o;
-  if (o.geometry != RT_GEOM_SPHERE || !o.transform || o.medium) return f;
+  if (!flattens(d, o)) return f;
   double cs, sn;
   rotate_y_cs(o, cs, sn);
   const double cx = o.p[0], cy = o.p[1], cz = o.p[2];
@@ -204,10 +224,20 @@ rt_object flat_object(const rt_object& o) {
 // A scene description whose objects are flat_object's (the objects live in `store`).
 rt_scene_desc flat_scene(const rt_scene_desc* d, std::vector<rt_object>& store) {
   store.resize((size_t)std::max(0, d->n_objects));
-  for (int i = 0; i < d->n_objects; ++i) store[i] = flat_object(d->objects[i]);
+  for (int i = 0; i < d->n_objects; ++i) store[i] = flat_object(d, d->objects[i]);
   rt_scene_desc f = *d;
   f.objects = store.data();
   return f;
+}
+// A flattened rotated sphere's u, v as its instance reports them (sphere.rs:17-26 on the object-frame
+// outward normal): the world normal rotated back by RotateY's inverse (rotate_y.h).
+void instance_sphere_uv(double cs, double sn, rt_hit& h) {
+  const double s = h.front_face ? 1.0 : -1.0;
+  const double nx = s * h.normal[0], ny = s * h.normal[1], nz = s * h.normal[2];
+  const double ox = cs * nx - sn * nz, oz = sn * nx + cs * nz;
+  const double pi = 3.14159265358979323846;
+  h.u = (std::atan2(-oz, ox) + pi) / (2.0 * pi);
+  h.v = std::acos(-ny) / pi;
 }
 // moving_sphere.h center(time), the device's formula (the bounding box uses it at time0 and time1)
 void moving_center(const rt_object& o, double tm, double* c) {
@@ -1157,6 +1187,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const uint64_t digest = scene_digest(d, builder);  // (of the description as given)
   std::vector<rt_object> flat;
   const rt_scene_desc fd = flat_scene(d, flat);
+  c->uv_fixups.clear();
+  for (int i = 0; i < d->n_objects; ++i)
+    if (d->objects[i].rotate_y_deg != 0.0 && flattens(d, d->objects[i])) {
+      double cs, sn;
+      rotate_y_cs(d->objects[i], cs, sn);
+      c->uv_fixups.push_back({i, {cs, sn}});
+    }
   d = &fd;
 
   BuiltTree tree = build_tree(d, builder);
@@ -1574,6 +1611,12 @@ int rt_scene_hit_ex(rt_ctx* c, const double* rays, int32_t n, double t_min, doub
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) st = fail(c, RT_E_HIP, "rt_scene_hit: %s", hipGetErrorString(e));
   }
+  if (!st && !c->uv_fixups.empty())  // (sorted by object index)
+    for (int32_t i = 0; i < n; ++i) {
+      auto it = std::lower_bound(c->uv_fixups.begin(), c->uv_fixups.end(), out[i].object,
+                                 [](const auto& f, int32_t o) { return f.first < o; });
+      if (it != c->uv_fixups.end() && it->first == out[i].object) instance_sphere_uv(it->second.first, it->second.second, out[i]);
+    }
   release(r);
   release(h);
   return st;

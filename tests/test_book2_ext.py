@@ -156,3 +156,43 @@ def test_final_scene_renders_on_oracle_with_light():
     cam = rt.scene_camera("final", 16, "square")
     img, cnt = O.OracleScene(s).render(cam, O.params(4, 50, 0x5EED))
     assert np.isfinite(img).all() and img.max() > 0 and cnt.samples == 16 * 16 * 4
+
+
+def rotated_sphere_scene():
+    """Two RotateY(40°)/Translate sphere instances: one earth-textured (its material reads u, v), one
+    solid (it does not).  ADVICE r05: flattening must not change what either reports."""
+    b = rt.SceneBuilder()
+    tr = rt.Transform(40.0, (0.5, 0.2, -0.3))
+    b.add(rt.Sphere((1.5, 0.0, 0.0), 1.0), rt.Lambertian(rt.TextureLoader.EarthBuiltin), transform=tr)
+    b.add(rt.Sphere((-2.0, 0.0, 1.0), 1.0), rt.Lambertian(rt.TextureLoader.solid(0.5, 0.5, 0.5)), transform=tr)
+    return b.finalize(1)
+
+
+def rotated_sphere_rays(n=512, seed=3):
+    rng = np.random.default_rng(seed)
+    orig = np.array([0.0, 0.5, 9.0]) + rng.normal(scale=0.3, size=(n, 3))
+    target = rng.uniform([-3.5, -1.5, -3.0], [2.5, 1.5, 1.5], size=(n, 3))
+    return np.hstack([orig, target - orig])
+
+
+def test_rotated_sphere_uv_is_the_instances():
+    """The scene query's u, v for both instances equal the per-ray instancing's (or_object_hit on the
+    instance: Translate then RotateY of the ray, sphere.rs:17-26 in the object frame).  The textured
+    instance is not flattened (bit-identical); the solid one is (t, u, v within rounding)."""
+    s = rotated_sphere_scene()
+    osc = O.OracleScene(s)
+    seen = {0: 0, 1: 0}
+    for ray in rotated_sphere_rays():
+        h = osc.hit(ray)
+        if not h.hit:
+            continue
+        seen[h.object] += 1
+        inst = hit(s.desc.objects[h.object], ray)
+        assert inst is not None
+        if h.object == 0:
+            assert (h.t, h.u, h.v) == (inst.t, inst.u, inst.v)
+            assert list(h.point) == list(inst.point) and list(h.normal) == list(inst.normal)
+        else:
+            assert abs(h.t - inst.t) <= 1e-12 * inst.t
+            assert abs(h.u - inst.u) < 1e-12 and abs(h.v - inst.v) < 1e-12
+    assert min(seen.values()) > 50

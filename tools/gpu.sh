@@ -4,7 +4,8 @@
 # the call (no further GPU work after a failure, a fault or a time limit).
 #
 # Steps (an argument "name" or "name:args", args split on blanks):
-#   tests[:pytest args]      pytest -m gpu (default: the whole suite; e.g. "tests:tests/test_gpu_ranges.py")
+#   tests[:pytest args]      the driver's `python -m pytest tests/ -x -q -m gpu`, clean env (e.g. "tests:tests/test_gpu_ranges.py")
+#   testsd[:pytest args]     the same, verbose, with per-test timeouts and a parity log
 #   testsv:<variant>[:args]  the same against exp/<variant>'s libraries (SHIRLEY_LIB_DIR)
 #   smoke                    __graft_entry__.smoke()
 #   bench[:bench.py args]    one bench line (default: the driver's defaults)
@@ -50,10 +51,15 @@ for step in "$@"; do
   [ "$name" != "$step" ] && args=${step#*:}
   log="$out/$(printf %02d $n)_$name.log"
   case $name in
-    tests)
-      timeout -k 10 900 python -u -m pytest ${args:-tests} -m gpu -x -v --timeout 120 --timeout-method thread \
-        -p no:cacheprovider > "$log" 2>&1
+    tests)  # the driver's own command (`python -m pytest tests/ -x -q -m gpu`, clean environment);
+            # the junit report only records per-test outcomes and times for profiles/<round>/
+      env -u SHIRLEY_LIB_DIR -u SHIRLEY_ASSETS -u SHIRLEY_PARITY_LOG timeout -k 10 900 python -m pytest ${args:-tests/} \
+        -x -q -m gpu --junitxml="$out/junit_$n.xml" > "$log" 2>&1
       rc=$?; echo "[$n tests] rc=$rc $(tail -1 "$log")" ;;
+    testsd)  # diagnostic form: verbose, per-test thread timeouts, parity log
+      SHIRLEY_PARITY_LOG=$PWD/$out/parity.jsonl timeout -k 10 900 python -u -m pytest ${args:-tests} -m gpu -x -v \
+        --timeout 120 --timeout-method thread -p no:cacheprovider > "$log" 2>&1
+      rc=$?; echo "[$n testsd] rc=$rc $(tail -1 "$log")" ;;
     testsv)  # testsv:<variant>[:pytest args] — the GPU tests against exp/<variant>'s libraries
       v=${args%%:*}
       targs=""
