@@ -1402,9 +1402,9 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   const long long stack_bytes = (long long)S.stack_depth * kTraceThreads * 8;
   const long long stack4_bytes = (long long)S.stack_depth4 * kTraceThreads * kStack4EntryBytes;
   // book-2 scenes: the EXT instance spills ~80 VGPRs at 4 waves per SIMD (1024 threads) and none at 3
-  // (768 threads, 165 VGPRs): final_scene +3.3 % (profiles/r02/wide3.txt).  SHIRLEY_WIDE4: tuning switch.
-  // The wide block's LDS holds the tree plus one stack per thread of the block actually launched.
-  const int wide_threads = (!exts.empty() && !getenv("SHIRLEY_WIDE4")) ? kTraceThreadsWide3 : kTraceThreadsWide;
+  // (768 threads, 165 VGPRs): final_scene +3.3 % (profiles/r02/wide3.txt), so no 1024-thread EXT instance
+  // is built.  The wide block's LDS holds the tree plus one stack per thread of the block actually launched.
+  const int wide_threads = !exts.empty() ? kTraceThreadsWide3 : kTraceThreadsWide;
   const long long wide_bytes =
       (long long)S.stack_depth4 * wide_threads * kStack4EntryBytes + (long long)nodes4.size() * n4_bytes;
   if (stack_bytes > kLdsBytes || stack4_bytes > kLdsBytes)

@@ -685,3 +685,28 @@ def test_collapse_choice_changes_nothing(gpu, monkeypatch, name, width, aspect):
     assert np.array_equal(frames["auto"], frames["1"])
     ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED), threads=16)
     check_parity(frames["auto"], ora, spp, frac_exact=PARITY_EXACT)
+
+
+def test_rotated_sphere_instances(gpu):
+    """a rotated sphere instance whose material reads u, v (earth texture) keeps per-ray
+    instancing; a rotated solid one is flattened, and rt_scene_hit still reports the instance's u, v
+    (object frame).  Query records and a frame against the oracle (which flattens by the same rule)."""
+    from test_book2_ext import rotated_sphere_rays, rotated_sphere_scene
+    scene = rotated_sphere_scene()
+    gpu.upload(scene)
+    rays = rotated_sphere_rays()
+    osc = O.OracleScene(scene)
+    seen = {0: 0, 1: 0}
+    for i, g in enumerate(gpu.hit(rays)):
+        h = osc.hit(rays[i], index=i)
+        assert g.object == (h.object if h.hit else -1), i
+        if g.object >= 0:
+            seen[g.object] += 1
+            assert abs(g.t - h.t) <= 1e-12 * h.t
+            assert abs(g.u - h.u) < 1e-12 and abs(g.v - h.v) < 1e-12
+    assert min(seen.values()) > 50
+    spp = 8
+    cam = rt.default_camera(32, "square")
+    ora, _ = osc.render(cam, O.params(spp, 50, SEED))
+    img = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp))
+    check_parity(img, ora, spp)
