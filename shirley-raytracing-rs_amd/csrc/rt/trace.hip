@@ -331,7 +331,7 @@ void trace_kernel(KParams P) {
       bool alive, has_emit = false;
       v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
       if (hit) {
-        const DMat m = mats[mat];
+        const DMat& m = mats[mat];  // (fields read where used: a copy loaded them all up front and spilled them)
         alive = shade_factor(S, texs, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
       } else {
         PH_COUNT(20);
@@ -699,7 +699,7 @@ __global__ __launch_bounds__(kHitThreads) void probe_kernel(DScene S, const doub
   bool alive = false, has_emit = false;
   v3 mul = V(1.0, 1.0, 1.0), emit = V(0.0, 0.0, 0.0);
   if (hit) {
-    const DMat m = S.mats[mat];
+    const DMat& m = S.mats[mat];
     alive = shade_factor(S, S.texs, m, leaf, pn, rs, un, rng, o, d, h, prim, face, mul, emit, has_emit);
     r.front_face = h.front_face ? 1 : 0;
     r.t = h.t;

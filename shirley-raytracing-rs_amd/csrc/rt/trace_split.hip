@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kTraceThreadsWide, 1) void split_kernel(KParams P) 
     if (active) {
       bool alive;
       if (hit) {
-        const DMat m = S.mats[mat];
+        const DMat& m = S.mats[mat];
         alive = shade_pre(S, m, leaf, pn, rs, un, rng, seed, o, d, h, prim, face, att, em);
       } else {
         em = em + hmul(att, sky_unit(S, un));

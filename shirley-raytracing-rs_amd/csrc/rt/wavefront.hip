@@ -279,7 +279,7 @@ __global__ __launch_bounds__(kGridThreads) void wf_shade(WfParams P) {
       Hit h;
       hit_record<false, EXT>(S, pr, face, o, d, t, rng, seed, h);
       hp = h.point;
-      const DMat m = S.mats[pr.material];
+      const DMat& m = S.mats[pr.material];
       if (m.kind == RT_MAT_DIELECTRIC) {  // dielectric.rs:21-49
         double ratio = h.front_face ? (1.0 / m.param) : m.param;
         v3 ud = unit(d);
