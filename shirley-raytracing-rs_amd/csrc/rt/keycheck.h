@@ -14,6 +14,10 @@
 // now; its peers, whose keys did not change, have already issued the frame's collectives, which the failed
 // rank never joins, so their stream waits there (they fail at their next call's deferred check, if their
 // host gets there).  Strict mode makes every rank fail in the call itself, at one host round trip per call.
+// A failed check (now or deferred) poisons the rank's communicator: its peers may still hold the failed
+// call's frame collectives on it, and a later all-gather from this rank would be paired with them
+// (mismatched types and sizes: undefined behaviour, not a stall).  So every later call on a poisoned
+// communicator fails at once and issues nothing; the program destroys and re-creates it.
 #pragma once
 
 #include <stdint.h>
@@ -24,6 +28,7 @@ struct KeyState {
   bool verified = false;      // the ranks agreed on verified_key at some call
   uint64_t verified_key = 0;
   bool pending = false;       // the previous call's gathered words are still to be checked
+  bool poisoned = false;      // a check failed: no further collective on this communicator
 };
 
 // Whether a call must check its own gathered words before issuing the frame's collectives.

@@ -84,10 +84,7 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   // ran 1490 Msamples/s with 256-unit windows and 1830-1880 with 64 (gpurun_out/r05a, r05f1); serving
   // just the pool's last 1 M units in 64-unit windows from a second counter did not help (r05f1: the
   // imbalance builds up over the whole frame, not at its end), nor did shrinking windows near the end.
-  {
-    const long long units = n_pix * (long long)P.n_chunks;
-    P.queue_window = (lanes > 0 && units >= 128 * lanes) ? kQueueWindow : kSegmentWindow;
-  }
+  // Each sample pass is its own launch with its own pool, so the rule counts a pass's units (below).
 
   // sample passes: at most `budget` bytes of [chunks][pixels][3] f64 partial sums per pass
   const long long chunk_bytes = std::max<long long>(1, n_pix * 3 * (long long)sizeof(double));
@@ -104,6 +101,10 @@ inline SamplePlan plan_samples(long long n_pix, int count, int engine, long long
   P.passes = (int)((P.n_chunks + per_pass - 1) / per_pass);
   P.per_pass = (P.n_chunks + P.passes - 1) / P.passes;  // even passes
   P.partial_bytes = std::max<long long>(1, n_pix * P.per_pass * 3) * (long long)sizeof(double);
+  {
+    const long long units = n_pix * (long long)P.per_pass;  // one pass's launch
+    P.queue_window = (lanes > 0 && units >= 128 * lanes) ? kQueueWindow : kSegmentWindow;
+  }
   return P;
 }
 

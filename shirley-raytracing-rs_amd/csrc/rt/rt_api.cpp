@@ -117,6 +117,8 @@ struct rt_ctx {
   std::vector<hipEvent_t> pass_ev;   // before / after the trace launch of each sample pass
   std::vector<KBlock> host_blocks;    // host sources of the device KBlocks (KParams.kconst)
   uint64_t digest = 0;               // rt_scene_digest of the uploaded scene
+  // device primitive number -> object index (primitives are numbered in the reference tree's leaf order)
+  std::vector<int32_t> prim_object;
   // flattened rotated spheres (flat_object): object index -> RotateY's cos, sin, for rt_scene_hit's u, v
   std::vector<std::pair<int32_t, std::pair<double, double>>> uv_fixups;
   uint64_t host_samples = 0;  // samples of a frame served without a trace kernel (max_depth == 0)
@@ -431,6 +433,29 @@ uint64_t scene_digest(const rt_scene_desc* d, int32_t builder) {
     f.bytes(m.rgb, (size_t)m.width * m.height * 3);
   }
   return f.h;
+}
+
+// Leaf order of a tree, lhs before rhs (in-order): rank[object]; objects outside it (a SAH tree leaves out
+// the never-hit inverted boxes) follow in index order.
+std::vector<int32_t> reference_ranks(const BuiltTree& t, int32_t n) {
+  std::vector<int32_t> rank((size_t)std::max(0, n), -1);
+  int32_t next = 0;
+  if (t.root >= 0) {
+    std::vector<int32_t> stack{t.root};
+    while (!stack.empty()) {
+      const BuildNode& nd = t.nodes[stack.back()];
+      stack.pop_back();
+      if (nd.leaf >= 0) {
+        if (rank[nd.leaf] < 0) rank[nd.leaf] = next++;
+        continue;
+      }
+      stack.push_back(nd.rhs);  // (popped after the whole lhs subtree)
+      stack.push_back(nd.lhs);
+    }
+  }
+  for (int32_t i = 0; i < n; ++i)
+    if (rank[i] < 0) rank[i] = next++;
+  return rank;
 }
 
 BuiltTree build_tree(const rt_scene_desc* d, int32_t builder) {
@@ -1197,6 +1222,25 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
   d = &fd;
 
   BuiltTree tree = build_tree(d, builder);
+  // Exact ties (rt_device.h tie_takes): the device numbers the primitives in the reference
+  // tree's leaf order, lhs before rhs (constructor.rs:9-36 via build_reference_tree), so that the lower
+  // number is the leaf the reference's rhs-first walk tests last; prim_object maps a number back.
+  std::vector<rt_object> ranked;
+  rt_scene_desc rd = *d;
+  {
+    const BuiltTree ref = builder == RT_BVH_REFERENCE ? tree : build_tree(d, RT_BVH_REFERENCE);
+    std::vector<int32_t> rank = reference_ranks(ref, d->n_objects);
+    ranked.resize((size_t)std::max(0, d->n_objects));
+    c->prim_object.assign((size_t)std::max(0, d->n_objects), 0);
+    for (int i = 0; i < d->n_objects; ++i) {
+      ranked[rank[i]] = d->objects[i];
+      c->prim_object[rank[i]] = i;
+    }
+    for (BuildNode& nd : tree.nodes)
+      if (nd.leaf >= 0) nd.leaf = rank[nd.leaf];
+    rd.objects = ranked.data();
+    d = &rd;
+  }
   std::vector<DNode> nodes;
   flatten(tree, nodes);
   std::vector<DNode4F> nodes4;
@@ -1241,6 +1285,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
         for (int k = 0; k < 3; ++k) e.off[k] = o.offset[k];
       }
       e.neg_inv_density = -1.0 / o.density;
+      e.object = c->prim_object[i];
       q.kind |= kPrimExt | (o.medium ? kPrimMedium : 0) | (o.transform ? kPrimXform : 0) |
                 ((int32_t)exts.size() << kPrimExtShift);
       exts.push_back(e);
@@ -1611,6 +1656,9 @@ int rt_scene_hit_ex(rt_ctx* c, const double* rays, int32_t n, double t_min, doub
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) st = fail(c, RT_E_HIP, "rt_scene_hit: %s", hipGetErrorString(e));
   }
+  if (!st)
+    for (int32_t i = 0; i < n; ++i)
+      if (out[i].object >= 0) out[i].object = c->prim_object[out[i].object];
   if (!st && !c->uv_fixups.empty())  // (sorted by object index)
     for (int32_t i = 0; i < n; ++i) {
       auto it = std::lower_bound(c->uv_fixups.begin(), c->uv_fixups.end(), out[i].object,
@@ -1642,6 +1690,9 @@ int rt_probe_segment(rt_ctx* c, const double* rays, int32_t n, uint64_t seed, ui
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     if (e != hipSuccess) st = fail(c, RT_E_HIP, "rt_probe_segment: %s", hipGetErrorString(e));
   }
+  if (!st)
+    for (int32_t i = 0; i < n; ++i)
+      if (out[i].object >= 0) out[i].object = c->prim_object[out[i].object];
   release(r);
   release(h);
   return st;
@@ -1933,6 +1984,7 @@ int check_call_key(rt_ctx* c, rt_comm* m, uint64_t key, hipStream_t s) {
     HIP_TRY(c, hipEventSynchronize(m->key_ev[m->key_pending]));
     if ((st = key_verdict(c, m->key_words + m->key_pending * slot_words, W))) {
       m->ks.verified = false;
+      m->ks.poisoned = true;
       return st;
     }
   }
@@ -1952,6 +2004,7 @@ int check_call_key(rt_ctx* c, rt_comm* m, uint64_t key, hipStream_t s) {
     HIP_TRY(c, hipEventSynchronize(m->key_ev[slot]));
     if ((st = key_verdict(c, hw, W))) {
       m->ks.verified = false;
+      m->ks.poisoned = true;
       return st;
     }
     m->ks.verified = true;
@@ -2016,6 +2069,8 @@ int rt_render_sharded(rt_ctx* c, rt_comm* m, const rt_camera* cam, const rt_rend
   if (!c) return RT_E_INVALID;
   if (!m || !m->comm) return fail(c, RT_E_INVALID, "no communicator");
   if (m->device != c->device) return fail(c, RT_E_INVALID, "communicator of device %d used with device %d", m->device, c->device);
+  if (m->ks.poisoned)  // (keycheck.h: its peers may still hold the failed call's frame collectives)
+    return fail(c, RT_E_INVALID, "communicator poisoned by a failed cross-rank check: destroy and re-create it");
   if (m->rank == 0 && !accum_dev) return fail(c, RT_E_INVALID, "accum_dev is NULL on the root");
   if (!c->have_scene) return fail(c, RT_E_INVALID, "no scene uploaded (call rt_scene_upload first)");
   if (!p || !cam) return fail(c, RT_E_INVALID, "camera/params is NULL");

@@ -586,7 +586,7 @@ __device__ __forceinline__ ExtHit ext_t(const DExt* exts, const double* shutter,
   if (t1 < 0.0) t1 = 0.0;
   const double ray_length = len(d);
   const double inside = (t2 - t1) * ray_length;
-  const double hd = e.neg_inv_density * RT_LOG(side_draw(seed, draw, sample, pixel, kStreamMedium | (uint32_t)prim));
+  const double hd = e.neg_inv_density * RT_LOG(side_draw(seed, draw, sample, pixel, kStreamMedium | (uint32_t)e.object));
   if (hd > inside) return r;
   const double th = t1 + hd / ray_length;
   if (th > t_max) return r;
@@ -742,6 +742,29 @@ __device__ __forceinline__ void hit_record(const DScene& S, const DPrim& pr, int
   else prim_record<WANT_UV>(pr, face, o, d, t, h);
 }
 
+// Exact ties.  Acceptance is inclusive (sphere.rs:40-45, rect.rs:58), so of primitives hit
+// at the same binary64 t the reference keeps the one its rhs-first walk (bbox_tree.rs:76-80) tests last:
+// the leftmost leaf of its own tree whose bounding box still passes hit2 at t_max = the tie (aabb.rs:74
+// rejects t_max <= t_min).  The host numbers the primitives in that leaf order (rt_api.cpp, reference
+// ranks), so for a candidate `leaf` hit at t == t_best against the current `best`:
+//   leaf < best — the candidate's box was just tested at t_max = t_best and passed: it wins;
+//   leaf > best — best wins unless its own box fails hit2 at t (re-tested from the global copy; ties only).
+__device__ __forceinline__ void leaf_box(const DPrim& pr, double* b);
+template <bool EXT>
+__device__ __forceinline__ bool tie_takes(const DScene& S, int leaf, int best, double t, double t_best, v3 o, v3 inv,
+                                          RaySigns ns, double t_min) {
+  if (t != t_best || (unsigned)leaf < (unsigned)best) return true;  // (best == -1: no hit yet)
+  const DPrim& pb = S.prims[best];
+  double b[6], te;
+  if (EXT && (pb.kind & kPrimExt)) {
+    const double* eb = S.exts[pb.kind >> kPrimExtShift].box;
+    for (int k = 0; k < 6; ++k) b[k] = eb[k];
+  } else {
+    leaf_box(pb, b);
+  }
+  return !slab_s(b, o, inv, ns, t_min, t, te);
+}
+
 // ------------------------------------------------------------------------------------------
 // BVH traversal: closest hit in [t_min, t_max] (bbox_tree.rs:56-91 semantics, near-first order)
 // ------------------------------------------------------------------------------------------
@@ -784,7 +807,8 @@ __device__ __forceinline__ void leaf_visit(const DScene& S, int prim, v3 o, v3 d
   double t;
   int f = -1;
   ++ptests;
-  if (prim_t<EXT>(S, pr, prim, o, d, T.a, t_min, T.t_best, rk, seed, t, f)) {
+  if (prim_t<EXT>(S, pr, prim, o, d, T.a, t_min, T.t_best, rk, seed, t, f) &&
+      tie_takes<EXT>(S, prim, T.best, t, T.t_best, o, T.inv, T.ns, t_min)) {
     T.t_best = t;
     T.best = prim;
     T.face = f;
@@ -867,7 +891,8 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
       double t;
       int f = -1;
       ++ptests;
-      if (prim_t<EXT>(S, pr, ~c0, o, d, a, t_min, t_best, rk, seed, t, f)) { t_best = t; best = ~c0; face_best = f; }
+      if (prim_t<EXT>(S, pr, ~c0, o, d, a, t_min, t_best, rk, seed, t, f) &&
+          tie_takes<EXT>(S, ~c0, best, t, t_best, o, inv, ns, t_min)) { t_best = t; best = ~c0; face_best = f; }
       h0 = false;
     }
     if (h1 && c1 < 0) {
@@ -875,7 +900,8 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
       double t;
       int f = -1;
       ++ptests;
-      if (prim_t<EXT>(S, pr, ~c1, o, d, a, t_min, t_best, rk, seed, t, f)) { t_best = t; best = ~c1; face_best = f; }
+      if (prim_t<EXT>(S, pr, ~c1, o, d, a, t_min, t_best, rk, seed, t, f) &&
+          tie_takes<EXT>(S, ~c1, best, t, t_best, o, inv, ns, t_min)) { t_best = t; best = ~c1; face_best = f; }
       h1 = false;
     }
     int next;
@@ -1098,8 +1124,8 @@ __device__ __forceinline__ void leaf_box(const DPrim& pr, double* b) {
 // evaluated object first — the same conjunction of two pure functions).  One loop per
 // leaf kind — spheres (sphere.rs:28-46), rects (rect.rs:54-65), boxes (rect.rs:132-156) — each in
 // child order, so a wave runs a kind's code only while one of its lanes holds a leaf of that kind.
-// (Which of several leaves with exactly equal t wins is the one tie the reference's own tree order
-// decides; see DESIGN.md.)  A hit also lowers tmaxf (the f32 bound of t_best the node tests use).
+// (Of several leaves with exactly equal t the reference's own leaf order decides: tie_takes.)  A hit also
+// lowers tmaxf (the f32 bound of t_best the node tests use).
 __device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
   const int lo = (k & 1) ? c1 : c0, hi = (k & 1) ? c3 : c2;
   return (k & 2) ? hi : lo;
@@ -1164,6 +1190,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       }
       if (!slab_sphere(pp->p, o, inv, ns, t_min, t_best)) continue;
     }
+    if (!tie_takes<EXT>(S, leaf, best, t, t_best, o, inv, ns, t_min)) continue;
     t_best = t; best = leaf; face_best = -1; hit = true;
   }
   // RectBox leaves before rect leaves: a box in front of a rect (the random scene's ground coat over its
@@ -1181,7 +1208,9 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       if (!slab_s(prim_ext(S, pr).box, o, inv, ns, t_min, t_best, te)) continue;
       RT_STAT(++ptests);
       int f = -1;
-      if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f)) { t_best = t; best = leaf; face_best = f; hit = true; }
+      if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f) && tie_takes<EXT>(S, leaf, best, t, t_best, o, inv, ns, t_min)) {
+        t_best = t; best = leaf; face_best = f; hit = true;
+      }
       continue;
     }
     // RT_BOX_TWO_PASS bits: box_t2 in the reference-scene (1) / book-2 (2) instances, box_t1f in the
@@ -1195,7 +1224,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     const int f = (kTwoPass && div_ok)   ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
                   : (kOneFull && div_ok) ? box_t1f(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
                                          : box_t(pr.p, o, d, t_min, t_best, t, inv, div_ok);
-    if (f >= 0) { t_best = t; best = leaf; face_best = f; hit = true; }
+    if (f >= 0 && tie_takes<EXT>(S, leaf, best, t, t_best, o, inv, ns, t_min)) { t_best = t; best = leaf; face_best = f; hit = true; }
   }
 #pragma unroll 1
   while (rect) {
@@ -1214,7 +1243,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       case kPrimRectYZ: h = rect_t<1, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok); break;
       default: h = rect_t<0, 2>(pr.p, o, d, t_min, t_best, t, inv, div_ok);
     }
-    if (h) { t_best = t; best = leaf; face_best = -1; hit = true; }
+    if (h && tie_takes<EXT>(S, leaf, best, t, t_best, o, inv, ns, t_min)) { t_best = t; best = leaf; face_best = -1; hit = true; }
   }
   if (hit) tmaxf = tmax_f32(t_best);
 }

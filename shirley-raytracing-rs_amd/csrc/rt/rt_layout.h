@@ -95,6 +95,8 @@ struct alignas(16) DExt {
   double cos_t, sin_t;      // RotateY: cos / sin of the angle in radians
   double off[3];            // Translate offset
   double neg_inv_density;   // ConstantMedium: -1 / density
+  int32_t object;           // the object's index in the scene description (its side-stream key; primitives
+  int32_t pad_;             //   are numbered by the reference's leaf order, rt_api.cpp)
 };
 static_assert(sizeof(DExt) == 144, "DExt layout");
 

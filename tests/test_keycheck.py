@@ -5,7 +5,8 @@ frames (one immediate check, then deferred ones: no host round trip), every rank
 together (checked in the call, on every rank), a genuine mismatch between ranks that all changed (every rank
 fails in the call, before any frame collective), and the misuse of one rank changing its key alone (that
 rank fails in the call; its peers fail at their next call's deferred check; strict mode fails them all in
-the call).  The reference loop this check guards is main.rs:117-125 (one process, no ranks)."""
+the call).  A failed check poisons the communicator: every later call on it fails at once and
+issues no collective, so no rank's all-gather is ever paired with a peer's pending frame collective.  The reference loop this check guards is main.rs:117-125 (one process, no ranks)."""
 import os
 import subprocess
 
@@ -29,9 +30,9 @@ def sim(tmp_path_factory):
 
 def test_steady_loop_checks_once_then_defers(sim):
     rows = sim(4, False, *[["a"] * 4] * 5)
-    assert rows[0] == ["S"] * 4 + ["gather=same"]
+    assert rows[0] == ["S"] * 4 + ["gather=same", "pairing=ok"]
     for r in rows[1:]:
-        assert r == ["A"] * 4 + ["gather=same"]
+        assert r == ["A"] * 4 + ["gather=same", "pairing=ok"]
 
 
 def test_all_ranks_change_together(sim):
@@ -44,28 +45,33 @@ def test_mismatch_after_a_common_change_fails_every_rank_in_the_call(sim):
     # all ranks change their arguments at call 2, rank 2 to different ones: every rank checks in the call
     # (its key is new) and fails naming rank 2, before any frame collective; a corrected call 3 agrees
     rows = sim(4, False, ["a"] * 4, ["a"] * 4, ["b", "b", "c", "b"], ["b"] * 4)
-    assert rows[2] == ["F2k"] * 4 + ["gather=same"]
-    assert rows[3] == ["S"] * 4 + ["gather=same"]
+    assert rows[2] == ["F2k"] * 4 + ["gather=same", "pairing=ok"]
+    # every rank's communicator is poisoned by the failed check: the corrected call must re-create it
+    assert rows[3] == ["X"] * 4 + ["gather=diverged", "pairing=ok"]
 
 
 def test_scene_mismatch_is_named_as_scene(sim):
     rows = sim(2, False, ["1:a", "2:a"])
-    assert rows[0] == ["F1s", "F1s", "gather=same"]
+    assert rows[0] == ["F1s", "F1s", "gather=same", "pairing=ok"]
 
 
 def test_lone_rank_change(sim):
     # misuse: rank 1 alone changes its key at call 2.  It checks in the call and fails; ranks 0 and 2 kept
     # their key, defer their check and issue the frame's collectives (which rank 1 never joins), then fail
     # at call 3's deferred check.  Every rank issued call 2's gather (one collective sequence).
-    rows = sim(3, False, ["a"] * 3, ["a"] * 3, ["a", "b", "a"], ["a", "b", "a"])
-    assert rows[2] == ["A", "F1k", "A", "gather=same"]
-    assert rows[3][0] == "P1k" and rows[3][2] == "P1k"
+    rows = sim(3, False, ["a"] * 3, ["a"] * 3, ["a", "b", "a"], ["a", "b", "a"], ["a", "b", "a"])
+    assert rows[2] == ["A", "F1k", "A", "gather=same", "pairing=ok"]
+    # call 3: rank 1's communicator is poisoned, so it issues no all-gather that ranks 0 and 2's queued
+    # frame collectives of call 2 could be paired with (round 5 issued one: undefined); 0 and 2 fail their
+    # deferred check, and from then on every rank fails at once
+    assert rows[3] == ["P1k", "X", "P1k", "gather=diverged", "pairing=ok"]
+    assert rows[4] == ["X", "X", "X", "gather=diverged", "pairing=ok"]
 
 
 def test_strict_mode_fails_every_rank_in_the_call(sim):
     rows = sim(3, True, ["a"] * 3, ["a"] * 3, ["a", "b", "a"])
     assert rows[0][:3] == rows[1][:3] == ["S"] * 3
-    assert rows[2] == ["F1k"] * 3 + ["gather=same"]
+    assert rows[2] == ["F1k"] * 3 + ["gather=same", "pairing=ok"]
 
 
 @pytest.mark.parametrize("world", [2, 5, 8])
@@ -82,3 +88,4 @@ def test_every_rank_sees_the_same_verdict_when_it_checks(sim, world):
     for call, row in zip(calls, rows):
         checked = [t for t in row[:world] if t[0] in "SF"]
         assert len(set(checked)) <= 1
+        assert row[-1] == "pairing=ok"  # never a collective paired with one of another kind

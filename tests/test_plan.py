@@ -155,3 +155,7 @@ def test_shared_queue_window_follows_units_per_lane(plan):
     assert below["queue_window"] == 64 and at["queue_window"] == 64  # (1 chunk: 2 units per lane)
     lo, hi = plan((pixels(1200, 800), 34, MEGA, LANES, 1, DEFAULT), (pixels(1200, 800), 35, MEGA, LANES, 1, DEFAULT))
     assert (lo["queue_window"], hi["queue_window"]) == (64, 256)  # 960000 x 34 < 128 x 262144 <= 960000 x 35
+    # a multi-pass frame: the rule counts one pass's units (each pass is its own launch and pool), so the
+    # 35-sample frame in passes of 7 chunks (< 128 units per lane each) takes 64-unit windows
+    split = plan((pixels(1200, 800), 35, MEGA, LANES, 1, pixels(1200, 800) * 24 * 7))
+    assert (split["passes"], split["per_pass"], split["queue_window"]) == (5, 7, 64)

@@ -7,9 +7,13 @@
 //   A  key unchanged: check deferred to the next call; frame collectives issued
 //   F<r><w>  check in the call failed (first differing rank r, w = s scene / k key): no frame collectives
 //   P<r><w>  the deferred check of the previous call failed: no gather, no frame collectives
-// followed by " gather=same" when every rank issued this call's all-gather, else " gather=diverged".
-// The simulation mirrors check_call_key in rt_api.cpp: deferred check, then the gather, then the
-// immediate check when key_check_now says so.
+//   X  the communicator is poisoned by an earlier failed check: the call fails at once, issues nothing
+// followed by " gather=same" when every rank issued this call's all-gather, else " gather=diverged", and
+// " pairing=ok" while every rank's sequence of issued collectives (all-gathers G, frame collectives F) is a
+// prefix of another's — RCCL then pairs like with like, and a rank that is behind only stalls its peers —,
+// else " pairing=mismatch" (a G paired with an F: undefined).
+// The simulation mirrors check_call_key and rt_render_sharded in rt_api.cpp: poisoned communicator, deferred
+// check, then the gather, then the immediate check when key_check_now says so, then the frame.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -27,6 +31,7 @@ int main(int argc, char** argv) {
   const bool strict = std::atoi(argv[2]) != 0;
   std::vector<rt::KeyState> ks(world);
   std::vector<std::vector<uint64_t>> pending_words(world);  // the words each rank's deferred check reads
+  std::vector<std::string> issued(world);                    // collectives each rank issued, in order
   for (int a = 3; a < argc; ++a) {
     std::vector<uint64_t> digest(world, 1), key(world, 0);
     std::string s = argv[a];
@@ -47,12 +52,18 @@ int main(int argc, char** argv) {
     std::vector<std::string> out(world);
     std::vector<bool> gathers(world, true);
     for (int r = 0; r < world; ++r) {
+      if (ks[r].poisoned) {
+        out[r] = "X";
+        gathers[r] = false;
+        continue;
+      }
       if (!ks[r].pending) continue;
       ks[r].pending = false;
       int what = 0;
       const int bad = rt::key_mismatch(pending_words[r].data(), world, &what);
       if (bad >= 0) {
         ks[r].verified = false;
+        ks[r].poisoned = true;
         out[r] = "P" + std::to_string(bad) + (what ? "k" : "s");
         gathers[r] = false;
       }
@@ -67,25 +78,36 @@ int main(int argc, char** argv) {
     for (int r = 0; r < world; ++r) all = all && gathers[r];
     for (int r = 0; r < world; ++r) {
       if (!gathers[r]) continue;
+      issued[r] += 'G';
       if (rt::key_check_now(ks[r], key[r], strict)) {
         int what = 0;
         const int bad = rt::key_mismatch(words.data(), world, &what);
         if (bad >= 0) {
           ks[r].verified = false;
+          ks[r].poisoned = true;
           out[r] = "F" + std::to_string(bad) + (what ? "k" : "s");
         } else {
           ks[r].verified = true;
           ks[r].verified_key = key[r];
           out[r] = "S";
+          issued[r] += 'F';
         }
       } else {
         ks[r].pending = true;
         pending_words[r] = words;
         out[r] = "A";
+        issued[r] += 'F';
       }
     }
+    bool pairing = true;
+    for (int a = 0; a < world; ++a)
+      for (int b = 0; b < world; ++b) {
+        const std::string& x = issued[a].size() <= issued[b].size() ? issued[a] : issued[b];
+        const std::string& y = issued[a].size() <= issued[b].size() ? issued[b] : issued[a];
+        pairing = pairing && y.compare(0, x.size(), x) == 0;
+      }
     for (int r = 0; r < world; ++r) std::printf("%s%s", r ? " " : "", out[r].c_str());
-    std::printf(" gather=%s\n", all ? "same" : "diverged");
+    std::printf(" gather=%s pairing=%s\n", all ? "same" : "diverged", pairing ? "ok" : "mismatch");
   }
   return 0;
 }
