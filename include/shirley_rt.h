@@ -350,7 +350,10 @@ int rt_probe_segment(rt_ctx* ctx, const double* rays, int32_t n, uint64_t seed, 
  * (ranks changing scene or arguments together all fail there with RT_E_INVALID on a mismatch); otherwise
  * at the rank's next call, so a loop of frames needs no host round trip.  Misuse — one rank changing its
  * key alone — fails that rank in the call; its peers have already issued the frame's collectives, which it
- * never joins, so their stream waits (undefined from RCCL's side: do not rely on it).  SHIRLEY_KEY_CHECK=sync
+ * never joins, so their stream waits (undefined from RCCL's side: do not rely on it).  A failed check poisons
+ * the communicator: every later rt_render_sharded call on it returns RT_E_INVALID and issues no collective
+ * (a new all-gather could otherwise be paired with a peer's pending frame collective); destroy it with
+ * rt_comm_destroy and create a new one.  SHIRLEY_KEY_CHECK=sync
  * checks every call before the frame's collectives (every rank fails in the call itself, one host round
  * trip per call).  rt_render_multi compares the digests on the host.  Replaces the
  * reference's whole-machine rayon loop over scanlines (main.rs:92-126).  RCCL is loaded on first use
