@@ -1286,6 +1286,7 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
       }
       e.neg_inv_density = -1.0 / o.density;
       e.object = c->prim_object[i];
+      e.prim = i;
       q.kind |= kPrimExt | (o.medium ? kPrimMedium : 0) | (o.transform ? kPrimXform : 0) |
                 ((int32_t)exts.size() << kPrimExtShift);
       exts.push_back(e);

@@ -1144,11 +1144,12 @@ __device__ __forceinline__ unsigned top_bytes(unsigned w0, unsigned w1, unsigned
   return __builtin_amdgcn_perm(w1, w0, 0x0c0c0703u) | __builtin_amdgcn_perm(w3, w2, 0x07030c0cu);
 }
 
-template <int MODE, bool EXT>
+template <int MODE, bool EXT, bool DEFER = false>
 __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_prims, v3 o, v3 d, v3 inv,
                                             RaySigns ns, const Recip& ra, bool ra_ok, double t_min, unsigned lm, int c0, int c1,
                                             int c2, int c3, const int32_t* chp, double& t_best, float& tmaxf, int& best,
-                                            int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests) {
+                                            int& face_best, const Rng& rk, uint64_t seed, unsigned& ptests,
+                                            unsigned& xdefer) {
   // lm: spread mask of hit leaf children (bit 8 i + 7: child i).  A leaf's child word is
   // ~(prim | flags), so its generic / box flags (bits 29 / 28) are bits 5 / 4 of its top byte, inverted.
   const unsigned nf = ~top_bytes((unsigned)c0, (unsigned)c1, (unsigned)c2, (unsigned)c3);
@@ -1206,6 +1207,13 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     double te, t;
     if (EXT && pr.kind != kPrimBox) {  // an extended primitive (book 2): exact box from its DExt record
       if (!slab_s(prim_ext(S, pr).box, o, inv, ns, t_min, t_best, te)) continue;
+      // DEFER: the object test after the traversal (ext_deferred) — it is a pure function of (ray, t_min,
+      // t_max), and a later, smaller t_max can only drop hits that lose anyway — so its code and registers
+      // stay out of the traversal loop (book-2 instances: 74 -> 26 spilled VGPRs at 4 waves per SIMD)
+      if (DEFER && (unsigned)(pr.kind >> kPrimExtShift) < 32u) {
+        xdefer |= 1u << (pr.kind >> kPrimExtShift);
+        continue;
+      }
       RT_STAT(++ptests);
       int f = -1;
       if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f) && tie_takes<EXT>(S, leaf, best, t, t_best, o, inv, ns, t_min)) {
@@ -1335,12 +1343,12 @@ __device__ __forceinline__ int node4_next(const DScene& S, int4 ch, float k0, fl
   top = stk[sp];
   return (int)(e & km);
 }
-template <int STRIDE, int MODE, bool EXT>
+template <int STRIDE, int MODE, bool EXT, bool DEFER = false>
 __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o, v3 d,
                                       v3 inv, RaySigns ns, const RayF& rf, const Recip& ra, bool ra_ok, double t_min, int node,
                                       double& t_best, float& tmaxf, int& best, int& face_best, int& sp,
                                       unsigned& top, unsigned* stk, const Rng& rk, uint64_t seed,
-                                      unsigned& visits, unsigned& ptests) {
+                                      unsigned& visits, unsigned& ptests, unsigned& xdefer) {
   int4 ch;
   float k0, k1, k2, k3;
   const int32_t* chp;
@@ -1348,9 +1356,33 @@ __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<E
                                         visits, chp);
   if (lm) PH_COUNT(1);
   if (lm)
-    leaf_tests4<MODE, EXT>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf, best,
-                           face_best, rk, seed, ptests);
+    leaf_tests4<MODE, EXT, DEFER>(S, lds_prims, o, d, inv, ns, ra, ra_ok, t_min, lm, ch.x, ch.y, ch.z, ch.w, chp, t_best, tmaxf,
+                                  best, face_best, rk, seed, ptests, xdefer);
   return node4_next<STRIDE, MODE != kSceneLds>(S, ch, k0, k1, k2, k3, tmaxf, sp, top, stk);
+}
+
+// The extended objects a traversal deferred (bit e: DScene.exts[e], whose box passed at its visit), each
+// tested against the final closest hit in index order — the same closest hit as testing them where they
+// were visited (each test is a pure function of the ray, t_min and t_max; ties: tie_takes).  Measured on
+// final_scene @ 200 spp: +2.7 % (1654 vs 1611); out of line (a call) -1.4 %, and a 1024-thread book-2
+// block (RT_EXT_WIDE_THREADS=1024, 4 waves per SIMD at 68-83 spilled VGPRs) -10 % (gpurun_out/r06g).
+__device__ __forceinline__ void ext_deferred(const DScene& S, unsigned xdefer, v3 o, v3 d, v3 inv, RaySigns ns,
+                                             double t_min, double& t_best, int& best, int& face_best, const Rng& rk,
+                                             uint64_t seed) {
+#pragma unroll 1
+  while (xdefer) {
+    const int e = __builtin_ctz(xdefer);
+    xdefer &= xdefer - 1u;
+    const int leaf = S.exts[e].prim;
+    const DPrim& pr = S.prims[leaf];
+    double t;
+    int f = -1;
+    if (ext_hit_t(S, pr, leaf, o, d, t_min, t_best, rk, seed, t, f) && tie_takes<true>(S, leaf, best, t, t_best, o, inv, ns, t_min)) {
+      t_best = t;
+      best = leaf;
+      face_best = f;
+    }
+  }
 }
 
 // Whole closest-hit query over the 4-wide tree (t_min > 0).  The conservative internal tests and the
@@ -1381,15 +1413,17 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
   int sp = 0;
   unsigned top = ~0u;  // the stack's top entry (node4_next)
   int node = S.root4;
+  unsigned xdefer = 0u;  // book-2: extended objects whose box passed, tested after the loop (leaf_tests4)
   // a tree traversal visits every node at most once: more steps than nodes can only be a defect,
   // and ends the loop instead of hanging the wave
   for (int steps = 0; steps < S.n_nodes4 && node >= 0; ++steps) {
 #ifdef RT_PHASE_TIMING
     ++g_trav_lane_steps;
 #endif
-    node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, ra, ra_ok, t_min, node, t_best, tmaxf, best,
-                                face_best, sp, top, stk, rk, seed, visits, ptests);
+    node = visit4<STRIDE, MODE, EXT, EXT>(S, lds_nodes, lds_prims, o, d, inv, ns, rf, ra, ra_ok, t_min, node, t_best, tmaxf,
+                                          best, face_best, sp, top, stk, rk, seed, visits, ptests, xdefer);
   }
+  if (EXT) ext_deferred(S, xdefer, o, d, inv, ns, t_min, t_best, best, face_best, rk, seed);
   return best;
 }
 
@@ -1430,8 +1464,9 @@ __device__ __forceinline__ bool trav4_step(const DScene& S, const typename Node4
                                            v3 d, double t_min, Trav4& T, unsigned* stk, const Rng& rk,
                                            uint64_t seed, unsigned& visits, unsigned& ptests) {
   if (++T.steps > S.n_nodes4) return true;  // defect guard
+  unsigned xdefer = 0u;  // (not used: the step-wise form tests extended objects at once)
   T.node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.ra, T.ra_ok, t_min, T.node, T.t_best,
-                                T.tmaxf, T.best, T.face, T.sp, T.top, stk, rk, seed, visits, ptests);
+                                     T.tmaxf, T.best, T.face, T.sp, T.top, stk, rk, seed, visits, ptests, xdefer);
   return T.node < 0;
 }
 

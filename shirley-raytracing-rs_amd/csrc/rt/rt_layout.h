@@ -16,7 +16,10 @@ constexpr int kTile = 8;
 constexpr int kTilePixels = kTile * kTile;  // == wavefront size
 constexpr int kTraceThreads = 256;      // megakernel block, BVH in L1/L2: 4 waves, several blocks per CU
 constexpr int kTraceThreadsWide = 1024; // megakernel block holding the whole BVH in LDS: 16 waves (4 per SIMD), one per CU
-constexpr int kTraceThreadsWide3 = 768; // the same at 3 waves per SIMD (168 VGPRs): book-2 (EXT) scenes
+#ifndef RT_EXT_WIDE_THREADS
+#define RT_EXT_WIDE_THREADS 768
+#endif
+constexpr int kTraceThreadsWide3 = RT_EXT_WIDE_THREADS;  // book-2 (EXT) scenes' wide block: 768 = 3 waves per SIMD (168 VGPRs)
 constexpr int kHitThreads = 256;    // rt_scene_hit kernel
 constexpr int kWave = 64;
 constexpr int kLdsBytes = 160 * 1024;  // LDS per CU (gfx950)
@@ -96,7 +99,8 @@ struct alignas(16) DExt {
   double off[3];            // Translate offset
   double neg_inv_density;   // ConstantMedium: -1 / density
   int32_t object;           // the object's index in the scene description (its side-stream key; primitives
-  int32_t pad_;             //   are numbered by the reference's leaf order, rt_api.cpp)
+                            //   are numbered by the reference's leaf order, rt_api.cpp)
+  int32_t prim;             // its primitive number (the deferred object tests, rt_device.h ext_deferred)
 };
 static_assert(sizeof(DExt) == 144, "DExt layout");
 

@@ -778,8 +778,8 @@ static hipError_t hit_prepare(const DScene& S) {
 hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
   hipError_t e = hit_prepare(S);
   if (e != hipSuccess) return e;
-  if (threads == kTraceThreadsWide) {  // reference scenes only: book-2 scenes take kTraceThreadsWide3
-    if (node_mode4(S) != kNodesLds || S.exts) return hipErrorInvalidValue;
+  if (threads == kTraceThreadsWide && !S.exts) {  // reference scenes only: book-2 scenes take kTraceThreadsWide3
+    if (node_mode4(S) != kNodesLds) return hipErrorInvalidValue;
     if (S.n_lds_prims > 0) return occupancy_impl1<kTraceThreadsWide, kSceneLds, false>(S, blocks_per_cu);
     return occupancy_impl1<kTraceThreadsWide, kNodesLds, false>(S, blocks_per_cu);
   }
@@ -798,8 +798,7 @@ hipError_t trace_occupancy(const DScene& S, int threads, int* blocks_per_cu) {
 hipError_t launch_trace(const KParams& p, int blocks, int threads, hipStream_t stream) {
   const size_t lds = trace_lds_bytes(p.scene.n_lds_nodes4, node4_bytes(p.scene.exts != nullptr), p.scene.n_lds_prims, p.scene.n_lds_perlin, p.scene.stack_depth4, threads,
                                      p.scene.n_lds_mats, p.scene.n_lds_texs);
-  if (threads == kTraceThreadsWide) {
-    if (p.scene.exts) return hipErrorInvalidValue;
+  if (threads == kTraceThreadsWide && !p.scene.exts) {
     if (p.scene.n_lds_prims > 0)
       hipLaunchKernelGGL((trace_kernel<kTraceThreadsWide, kSceneLds, false>), dim3(blocks), dim3(threads), lds, stream, p);
     else
