@@ -145,10 +145,11 @@ void trace_kernel(KParams P) {
 #if defined(RT_PHASE_TIMING) && !defined(RT_PHASE_NO_EVENTS)
     const unsigned long long ph_before = ph_lane_steps;
 #endif
-    // the scene record: book-2 instances read it with scalar loads from the pass's KBlock in each
-    // iteration, so its pointers are not held in SGPRs across the loop (the 768-thread instance's SGPR
-    // spills 50 -> 25, final_scene +0.2 %: DESIGN.md §5); reference scenes keep the kernel argument
-    const DScene& S = EXT ? *(const DScene*)&kblock(P.kconst)->scene : P.scene;
+    // the scene record: the kernel argument's copy for every instance.  (Round 5 had the book-2 instances
+    // re-read it from the pass's KBlock with scalar loads each iteration, +0.2 % then; with the extended
+    // objects' tests moved out of the traversal loop the argument copy is +1.1 % on final_scene:
+    // 1675 / 1676 vs 1657 / 1655 Msamples/s, gpurun_out/r06n)
+    const DScene& S = P.scene;
     // 1. one ray_color iteration (render.rs:30-46): closest hit and hit record, the material and the
     // texture leaf of a diffuse / emitting material
     bool hit = false, need_pn = false, need_r = false;
