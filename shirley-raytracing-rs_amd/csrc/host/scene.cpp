@@ -1,7 +1,6 @@
 // scene.cpp — SceneBuilder model, serde-JSON interchange, finalize (texture load + Perlin tables).
 #include "scene.hpp"
 
-#include <dlfcn.h>
 #include <zlib.h>
 
 #include <cinttypes>
@@ -511,20 +510,26 @@ struct Loader {
   uint64_t seed;
   std::map<std::string, int32_t> image_cache;  // identical files share texels (no semantic change)
 
-  // path "" = EarthBuiltin (embedded texels), anything else a user file (ImagePath)
-  int32_t image(const std::string& path) {
-    auto it = image_cache.find(path);
-    if (it != image_cache.end()) return it->second;
+  int32_t earth_image = -1;  // EarthBuiltin's image, once loaded (the embedded texels, earth_embed.S)
+
+  // builtin: EarthBuiltin; else `path` names a user file (ImagePath)
+  int32_t image(const std::string& path, bool builtin = false) {
+    if (builtin && earth_image >= 0) return earth_image;
+    if (!builtin) {
+      auto it = image_cache.find(path);
+      if (it != image_cache.end()) return it->second;
+    }
     int32_t w = 0, h = 0;
     std::vector<uint8_t> px;
     std::string err;
-    bool ok = path.empty() ? load_earth_builtin(&w, &h, &px, &err) : load_image_file(path, &w, &h, &px, &err);
+    bool ok = builtin ? load_earth_builtin(&w, &h, &px, &err) : load_image_file(path, &w, &h, &px, &err);
     if (!ok) throw std::runtime_error(err);
     d.image_pixels.push_back(std::move(px));
     rt_image im{w, h, nullptr};
     d.images.push_back(im);
     int32_t idx = (int32_t)d.images.size() - 1;
-    image_cache[path] = idx;
+    if (builtin) earth_image = idx;
+    else image_cache[path] = idx;
     return idx;
   }
 
@@ -548,7 +553,7 @@ struct Loader {
       }
       case TextureLoader::EarthBuiltin:
         x.kind = RT_TEX_IMAGE;
-        x.table = image("");
+        x.table = image(std::string(), true);
         break;
       case TextureLoader::ImagePath:
         x.kind = RT_TEX_IMAGE;
