@@ -742,18 +742,53 @@ __device__ __forceinline__ void hit_record(const DScene& S, const DPrim& pr, int
   else prim_record<WANT_UV>(pr, face, o, d, t, h);
 }
 
-// Exact ties.  Acceptance is inclusive (sphere.rs:40-45, rect.rs:58), so of primitives hit
-// at the same binary64 t the reference keeps the one its rhs-first walk (bbox_tree.rs:76-80) tests last:
-// the leftmost leaf of its own tree whose bounding box still passes hit2 at t_max = the tie (aabb.rs:74
-// rejects t_max <= t_min).  The host numbers the primitives in that leaf order (rt_api.cpp, reference
-// ranks), so for a candidate `leaf` hit at t == t_best against the current `best`:
+// Exact ties.  Acceptance is inclusive (sphere.rs:40-45, rect.rs:58) and bbox_tree.rs:56-91
+// walks the reference tree rhs-first, re-testing every node and leaf box against the running closest with
+// hit2's strict `t_max <= t_min` (aabb.rs:74).  So of the objects hit at the closest binary64 t*, the first
+// the reference meets is the one latest in its tree's leaf order (lhs before rhs), and each later one — each
+// earlier in leaf order — replaces it iff its own box still passes hit2 at t* (its ancestors' boxes contain
+// it, so they pass too).  The winner: the earliest in leaf order whose box passes at t*, else the latest.
+// The host numbers the primitives in that leaf order (rt_api.cpp reference_ranks), so it is a function of
+// the set of tied primitives, whatever tree the device walks and in whatever order: the order "box passes
+// at t*, lowest rank first; then the others, highest rank first" is total, so the winner can be kept
+// incrementally.  Two tested candidates at an equal t are compared at once (tie_takes).  A tied object
+// whose own test is skipped because its box fails at the running closest (near_entry: by no more than
+// rounding; a sphere, whose t is known before its box test, on t == t_best exactly) raises `tie`, and a
+// traversal that ends with `tie` set recomputes the winner over every primitive (resolve_ties: rare, exact).
+__device__ __forceinline__ void leaf_box(const DPrim& pr, double* b);
+// A box that fails hit2 at the running closest t_best with its entry te only slightly beyond it may still
+// hold a primitive hit at exactly t_best: a RectBox's face t is the correctly rounded (b - o) / d and its
+// slab entry (b - o) * (1 / d), a few ulps apart.  Such a failure raises `tie` when te lies in the same or
+// the next high word as t_best (both >= 0 order like their bit patterns): within 2^-19 relative, far above
+// any rounding gap, in two instructions (a 64-bit ulp count cost Cornell 0.3-0.6 %, r06aa / r06ab).  The
+// band reaches a little below t_best too (a box missed with its entry there): those marks, like any in the
+// band without a tie, only run resolve_ties for nothing.
+__device__ __forceinline__ bool near_entry(double te, double t_best) {
+  return (unsigned)__double2hiint(te) - (unsigned)__double2hiint(t_best) <= 1u;
+}
+// `tie` is bit 30 of the running best primitive (indices stay below 2^28, kLeafPrimMask): a vector bit
+// that a new closest hit clears by assignment, where a separate per-lane flag would hold an SGPR pair
+// through the whole traversal loop (the megakernels' SGPRs are at the limit).  best = -1 is unchanged by it.
+constexpr int kTieBit = 1 << 30;
+// (reference-scene instances only: book-2 scenes, parity unpinned, keep the pairwise rule of tie_takes —
+// there the marks and the resolve pass cost final_scene 4.6 %, r06y)
+template <bool EXT>
+__device__ __forceinline__ void mark_tie(int& best, bool c) {
+  if constexpr (!EXT) best |= c ? kTieBit : 0;
+}
+__device__ __forceinline__ int strip_tie(int best) { return best < 0 ? best : (best & ~kTieBit); }
+// Closest-hit update of an accepted object hit (t <= t_best).  Strictly closer, or the first hit at all
+// (best = -1: the reference accepts t == t_max), replaces.  An equal t between two primitives whose boxes
+// both passed is decided at once by the rank order (both are candidates the reference tests):
 //   leaf < best — the candidate's box was just tested at t_max = t_best and passed: it wins;
 //   leaf > best — best wins unless its own box fails hit2 at t (re-tested from the global copy; ties only).
-__device__ __forceinline__ void leaf_box(const DPrim& pr, double* b);
+// (While `tie` is set resolve_ties decides at the end, so the pair is left alone.)
 template <bool EXT>
 __device__ __forceinline__ bool tie_takes(const DScene& S, int leaf, int best, double t, double t_best, v3 o, v3 inv,
                                           RaySigns ns, double t_min) {
-  if (t != t_best || (unsigned)leaf < (unsigned)best) return true;  // (best == -1: no hit yet)
+  if (t != t_best || best < 0) return true;
+  if (best & kTieBit) return false;
+  if (leaf < best) return true;
   const DPrim& pb = S.prims[best];
   double b[6], te;
   if (EXT && (pb.kind & kPrimExt)) {
@@ -763,6 +798,80 @@ __device__ __forceinline__ bool tie_takes(const DScene& S, int leaf, int best, d
     leaf_box(pb, b);
   }
   return !slab_s(b, o, inv, ns, t_min, t, te);
+}
+template <bool EXT>
+__device__ __forceinline__ bool prim_t(const DScene& S, const DPrim& pr, int prim, v3 o, v3 d, double a,
+                                       double t_min, double t_max, const Rng& rk, uint64_t seed, double& t,
+                                       int& face);
+// (inline; RT_TIES_OUTLINE makes it a call — -0.3 % on Cornell / headline, r06aa — for which the scene
+// pointers and the seed, launch-uniform, are read back as such for the side streams' SGPR-pinned keys)
+struct TieWin {
+  int best, face;
+};
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+}
+template <class T>
+__device__ __forceinline__ T* uniform_ptr(T* p) {
+  return (T*)(uintptr_t)uniform64((uint64_t)(uintptr_t)p);
+}
+#ifdef RT_TIES_OUTLINE
+#define RT_TIES_LINKAGE __noinline__
+#else
+#define RT_TIES_LINKAGE __forceinline__
+#endif
+template <bool EXT>
+__device__ RT_TIES_LINKAGE TieWin resolve_ties_ool(const DPrim* prims_v, const DExt* exts_v, const double* shutter_v,
+                                                int n_prims, v3 o, v3 d, double t_min, double ts, Rng rk,
+                                                uint64_t seed_v) {
+  DScene S{};
+  S.prims = uniform_ptr(prims_v);
+  S.exts = uniform_ptr(exts_v);
+  S.shutter = uniform_ptr(shutter_v);
+  const uint64_t seed = uniform64(seed_v);
+  n_prims = __builtin_amdgcn_readfirstlane(n_prims);
+  // the ray's reciprocals and |d|^2 recomputed (the same correctly rounded values the traversal used), so
+  // that the callers' copies need not outlive their loops
+  const v3 inv = V(1.0 / d.x, 1.0 / d.y, 1.0 / d.z);
+  const RaySigns ns = ray_signs(inv);
+  const double a = len2(d);
+  int pmin = -1, pface = -1, mmax = -1, mface = -1;
+#pragma unroll 1
+  for (int i = 0; i < n_prims; ++i) {
+    const DPrim& pr = S.prims[i];
+    double b[6], t, te;
+    if (EXT && (pr.kind & kPrimExt)) {
+      const double* eb = S.exts[pr.kind >> kPrimExtShift].box;
+      for (int k = 0; k < 6; ++k) b[k] = eb[k];
+    } else {
+      leaf_box(pr, b);
+    }
+    // (the box first: one entered well beyond ts holds no primitive hit at ts — the margin 2^-16 is far
+    // above any rounding gap between a primitive's t and its box, and above near_entry's band)
+    if (!slab_s(b, o, inv, ns, t_min, __builtin_inf(), te) || te > fma(ts, 0x1p-16, ts)) continue;
+    int f = -1;
+    if (!prim_t<EXT>(S, pr, i, o, d, a, t_min, ts, rk, seed, t, f) || t != ts) continue;
+    mmax = i;  // (ascending: the latest in leaf order so far)
+    mface = f;
+    if (pmin < 0 && slab_s(b, o, inv, ns, t_min, ts, te)) {
+      pmin = i;
+      pface = f;
+    }
+  }
+  return pmin >= 0 ? TieWin{pmin, pface} : TieWin{mmax, mface};
+}
+template <bool EXT>
+__device__ __forceinline__ void resolve_ties(const DScene& S, v3 o, v3 d, double t_min, double ts, int& best,
+                                             int& face_best, const Rng& rk, uint64_t seed) {
+  if constexpr (EXT) return;  // (nothing marks a book-2 traversal: mark_tie)
+  if (best < 0 || !(best & kTieBit)) return;
+  best &= ~kTieBit;
+  const TieWin w = resolve_ties_ool<EXT>(S.prims, S.exts, S.shutter, S.n_prims, o, d, t_min, ts, rk, seed);
+  if (w.best >= 0) {
+    best = w.best;
+    face_best = w.face;
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -774,7 +883,7 @@ struct Trav {
   RaySigns ns;    // 1/d < 0 per axis
   double a;       // |d|^2 (sphere.rs:31)
   double t_best;  // closest accepted t so far (t_max initially)
-  int best, face, node, sp, steps;
+  int best, face, node, sp, steps;  // best: | kTieBit while an exact tie at t_best may be unresolved
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, v3 d, double t_max) {
@@ -824,13 +933,18 @@ template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_nodes, v3 o, v3 d, double t_min, Trav& T,
                                           const Rng& rk, uint64_t seed, int* stk_node, float* stk_t,
                                           unsigned& visits, unsigned& ptests) {
-  if (++T.steps > S.n_nodes) return true;  // defect guard: a traversal visits each node at most once
+  if (++T.steps > S.n_nodes) {  // defect guard: a traversal visits each node at most once
+    T.best = strip_tie(T.best);
+    return true;
+  }
   const DNode& nd = fetch_node<MODE>(S, lds_nodes, T.node);
   const int c0 = nd.child[0], c1 = nd.child[1];
   double te0 = 0.0, te1 = 0.0;
   bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, T.inv, T.ns, t_min, T.t_best, te0);
   bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, T.inv, T.ns, t_min, T.t_best, te1);
   visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
+  // a box failing at the closest t by no more than rounding: a possible tie below it (near_entry)
+  mark_tie<EXT>(T.best, (!h0 && near_entry(te0, T.t_best)) || (!h1 && near_entry(te1, T.t_best)));
   // leaf children (one primitive each)
   if (h0 && c0 < 0) {
     leaf_visit<EXT>(S, ~c0, o, d, t_min, T, rk, seed, ptests);
@@ -859,7 +973,10 @@ __device__ __forceinline__ bool trav_step(const DScene& S, const DNode* lds_node
         break;
       }
     }
-    if (next < 0) return true;
+    if (next < 0) {
+      resolve_ties<EXT>(S, o, d, t_min, T.t_best, T.best, T.face, rk, seed);
+      return true;
+    }
   }
   T.node = next;
   return false;
@@ -886,13 +1003,18 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
     bool h0 = (c0 != kEmptyChild) && slab_s(nd.box[0], o, inv, ns, t_min, t_best, te0);
     bool h1 = (c1 != kEmptyChild) && slab_s(nd.box[1], o, inv, ns, t_min, t_best, te1);
     visits += (c0 != kEmptyChild ? 1u : 0u) + (c1 != kEmptyChild ? 1u : 0u);
+    mark_tie<EXT>(best, (!h0 && near_entry(te0, t_best)) || (!h1 && near_entry(te1, t_best)));
     if (h0 && c0 < 0) {
       const DPrim& pr = S.prims[~c0];
       double t;
       int f = -1;
       ++ptests;
       if (prim_t<EXT>(S, pr, ~c0, o, d, a, t_min, t_best, rk, seed, t, f) &&
-          tie_takes<EXT>(S, ~c0, best, t, t_best, o, inv, ns, t_min)) { t_best = t; best = ~c0; face_best = f; }
+          tie_takes<EXT>(S, ~c0, best, t, t_best, o, inv, ns, t_min)) {
+        t_best = t;
+        best = ~c0;
+        face_best = f;
+      }
       h0 = false;
     }
     if (h1 && c1 < 0) {
@@ -901,7 +1023,11 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
       int f = -1;
       ++ptests;
       if (prim_t<EXT>(S, pr, ~c1, o, d, a, t_min, t_best, rk, seed, t, f) &&
-          tie_takes<EXT>(S, ~c1, best, t, t_best, o, inv, ns, t_min)) { t_best = t; best = ~c1; face_best = f; }
+          tie_takes<EXT>(S, ~c1, best, t, t_best, o, inv, ns, t_min)) {
+        t_best = t;
+        best = ~c1;
+        face_best = f;
+      }
       h1 = false;
     }
     int next;
@@ -928,6 +1054,7 @@ __device__ __forceinline__ int traverse(const DScene& S, const DNode* lds_nodes,
     }
     node = next;
   }
+  resolve_ties<EXT>(S, o, d, t_min, t_best, best, face_best, rk, seed);
   return best;
 }
 
@@ -1124,7 +1251,8 @@ __device__ __forceinline__ void leaf_box(const DPrim& pr, double* b) {
 // evaluated object first — the same conjunction of two pure functions).  One loop per
 // leaf kind — spheres (sphere.rs:28-46), rects (rect.rs:54-65), boxes (rect.rs:132-156) — each in
 // child order, so a wave runs a kind's code only while one of its lanes holds a leaf of that kind.
-// (Of several leaves with exactly equal t the reference's own leaf order decides: tie_takes.)  A hit also
+// (Of several leaves hit at exactly the closest t the reference's own leaf order decides: tie_takes, resolve_ties.)
+// A hit also
 // lowers tmaxf (the f32 bound of t_best the node tests use).
 __device__ __forceinline__ int child_at(int k, int c0, int c1, int c2, int c3) {
   const int lo = (k & 1) ? c1 : c0, hi = (k & 1) ? c3 : c2;
@@ -1189,7 +1317,10 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
       } else {
         asm volatile("" : "+v"(pp));
       }
-      if (!slab_sphere(pp->p, o, inv, ns, t_min, t_best)) continue;
+      if (!slab_sphere(pp->p, o, inv, ns, t_min, t_best)) {
+        mark_tie<EXT>(best, t == t_best);  // (a sphere at the closest t whose box fails there: a possible tie)
+        continue;
+      }
     }
     if (!tie_takes<EXT>(S, leaf, best, t, t_best, o, inv, ns, t_min)) continue;
     t_best = t; best = leaf; face_best = -1; hit = true;
@@ -1206,7 +1337,7 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double te, t;
     if (EXT && pr.kind != kPrimBox) {  // an extended primitive (book 2): exact box from its DExt record
-      if (!slab_s(prim_ext(S, pr).box, o, inv, ns, t_min, t_best, te)) continue;
+      if (!slab_s(prim_ext(S, pr).box, o, inv, ns, t_min, t_best, te)) continue;  // (no tie marks: mark_tie)
       // DEFER: the object test after the traversal (ext_deferred) — it is a pure function of (ray, t_min,
       // t_max), and a later, smaller t_max can only drop hits that lose anyway — so its code and registers
       // stay out of the traversal loop (book-2 instances: 74 -> 26 spilled VGPRs at 4 waves per SIMD)
@@ -1227,7 +1358,10 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     // (the scene-in-LDS instances only: compiled into the L1/L2 ones it cost gen_spheres 0.7 %)
     constexpr bool kOneFull = (RT_BOX_TWO_PASS & (EXT ? 8 : 4)) != 0 && (EXT || MODE == kSceneLds);
     double tx;
-    if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te, tx)) continue;  // a RectBox's bounding box is its p[0..5]
+    if (!slab_s(pr.p, o, inv, ns, t_min, t_best, te, tx)) {  // a RectBox's bounding box is its p[0..5]
+      mark_tie<EXT>(best, near_entry(te, t_best));
+      continue;
+    }
     RT_STAT(++ptests);
     const int f = (kTwoPass && div_ok)   ? box_t2(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
                   : (kOneFull && div_ok) ? box_t1f(pr.p, o, d, inv, ns, t_min, t_best, te, tx, t)
@@ -1243,6 +1377,8 @@ __device__ __forceinline__ void leaf_tests4(const DScene& S, const DPrim* lds_pr
     const DPrim& pr = (MODE == kSceneLds) ? lds_prims[leaf] : S.prims[leaf];
     double b[6], te, t;
     leaf_box(pr, b);
+    // (no tie mark: the box is padded 0.0001 along the normal, so it fails at the rect's own t only where
+    // that t is on the rect's edge, a rounding-level coincidence; the mark cost Cornell 1.5 %, r06z)
     if (!slab_s(b, o, inv, ns, t_min, t_best, te)) continue;
     RT_STAT(++ptests);
     bool h;
@@ -1366,9 +1502,8 @@ __device__ __forceinline__ int visit4(const DScene& S, const typename Node4Sel<E
 // were visited (each test is a pure function of the ray, t_min and t_max; ties: tie_takes).  Measured on
 // final_scene @ 200 spp: +2.7 % (1654 vs 1611); out of line (a call) -1.4 %, and a 1024-thread book-2
 // block (RT_EXT_WIDE_THREADS=1024, 4 waves per SIMD at 68-83 spilled VGPRs) -10 % (gpurun_out/r06g).
-__device__ __forceinline__ void ext_deferred(const DScene& S, unsigned xdefer, v3 o, v3 d, v3 inv, RaySigns ns,
-                                             double t_min, double& t_best, int& best, int& face_best, const Rng& rk,
-                                             uint64_t seed) {
+__device__ __forceinline__ void ext_deferred(const DScene& S, unsigned xdefer, v3 o, v3 d, v3 inv, RaySigns ns, double t_min, double& t_best,
+                                             int& best, int& face_best, const Rng& rk, uint64_t seed) {
 #pragma unroll 1
   while (xdefer) {
     const int e = __builtin_ctz(xdefer);
@@ -1424,6 +1559,8 @@ __device__ __forceinline__ int traverse4(const DScene& S, const typename Node4Se
                                           best, face_best, sp, top, stk, rk, seed, visits, ptests, xdefer);
   }
   if (EXT) ext_deferred(S, xdefer, o, d, inv, ns, t_min, t_best, best, face_best, rk, seed);
+  if (best >= 0 && (best & kTieBit)) PH_COUNT(25);
+  resolve_ties<EXT>(S, o, d, t_min, t_best, best, face_best, rk, seed);
   return best;
 }
 
@@ -1463,11 +1600,16 @@ template <int STRIDE, int MODE, bool EXT>
 __device__ __forceinline__ bool trav4_step(const DScene& S, const typename Node4Sel<EXT>::T* lds_nodes, const DPrim* lds_prims, v3 o,
                                            v3 d, double t_min, Trav4& T, unsigned* stk, const Rng& rk,
                                            uint64_t seed, unsigned& visits, unsigned& ptests) {
-  if (++T.steps > S.n_nodes4) return true;  // defect guard
+  if (++T.steps > S.n_nodes4) {  // defect guard
+    T.best = strip_tie(T.best);
+    return true;
+  }
   unsigned xdefer = 0u;  // (not used: the step-wise form tests extended objects at once)
   T.node = visit4<STRIDE, MODE, EXT>(S, lds_nodes, lds_prims, o, d, T.inv, T.ns, T.rf, T.ra, T.ra_ok, t_min, T.node, T.t_best,
                                      T.tmaxf, T.best, T.face, T.sp, T.top, stk, rk, seed, visits, ptests, xdefer);
-  return T.node < 0;
+  if (T.node >= 0) return false;
+  resolve_ties<EXT>(S, o, d, t_min, T.t_best, T.best, T.face, rk, seed);
+  return true;
 }
 
 template <int MODE, class N4>

@@ -977,8 +977,8 @@ void phase_counters_dump() {
                                 "pop_iter", "segment_iter", "box_iter", "marble_round", "draws_coop_round",
                                 "unit_fetch", "camera_ray", "philox_A", "philox_B", "marble_sin", "hit_record",
                                 "checker_level", "dielectric", "metal", "lambertian", "sky", "diffuse_light",
-                                "reflectance", "traverse4", "publish"};
-  for (int i = 0; i < 25; ++i)
+                                "reflectance", "traverse4", "publish", "tie_resolve"};
+  for (int i = 0; i < 26; ++i)
     if (h[2 * i + 1])
       fprintf(stderr, "[phase-ev] %-18s lanes %.4g waves %.4g lanes/wave %.2f\n", names[i], (double)h[2 * i],
               (double)h[2 * i + 1], (double)h[2 * i] / (double)h[2 * i + 1]);

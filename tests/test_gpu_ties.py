@@ -4,9 +4,11 @@ The reference accepts a hit at t == the running closest t (sphere.rs:40-45 rejec
 rect.rs:58 only `t > t_max`), so the tied primitive tested LAST wins — provided its bounding box passes
 `hit2` (aabb.rs:62-79), whose `t_max <= t_min` test is strict, at t_max = the tie.  bbox_tree.rs:56-91
 pops rhs before lhs, so the last one tested is the leftmost leaf of the reference tree whose box passes.
-The device numbers its primitives in that leaf order (rt_api.cpp reference_ranks) and breaks an equal t
-by it, re-testing the current best's box at the tie when a higher-numbered primitive ties it
-(rt_device.h tie_takes) — whatever tree it traverses (SAH by default) and in whatever order.
+The device numbers its primitives in that leaf order (rt_api.cpp reference_ranks) and compares two tested
+candidates at an equal t by it (rt_device.h tie_takes); a traversal that skipped a box failing at the
+closest t by no more than rounding re-decides the winner once at its end from all tied primitives
+(resolve_ties; the rule is pinned on CPU in test_tie_rule.py) — whatever tree it traverses (SAH by
+default) and in whatever order.
 No reference scene produces a tie (the random scene's coat, y in [-0.01, 0], lies 0.01 above its lower
 surface at y = -0.02: scenes.rs:251-279; the Cornell walls meet only at edges).  Constructed here: two
 coincident spheres, and an xz_rect coplanar with a RectBox's top face.  The tests assert the reference's
@@ -128,3 +130,48 @@ def test_rect_coplanar_with_rectbox_face_tie(gpu, bvh):
         dep, exact = _frame_departure(gpu, scene, cam)
         _log(f"ties:rect_on_rectbox_face_frame:{order}", departure_px=dep, exact=exact)
         assert dep <= 0.001 and exact >= 0.99  # (round 5: 11.7 % departed with the box first)
+
+
+@pytest.mark.parametrize("bvh", ["reference", "sah"])
+def test_every_hit_a_tie_matches_the_reference(gpu, bvh):
+    """random_scene with every object twice — the copy right after the original, with a red Lambertian
+    instead of the original material — so that every hit of every path is an exact tie between two
+    primitives, and the winner decides the colour and the path.  The frame must follow the reference's
+    choice (the oracle walks the reference tree rhs-first, bbox_tree.rs:76-80) on both trees the device
+    can walk; round 5's device chose by its own test order here."""
+    from test_gpu_parity import check_parity
+    src = json.loads(rt.scenes.random_scene(SEED).to_json())
+    red = {"Lambertian": {"albedo": {"Solid": {"vec": [0.9, 0.1, 0.05]}}}}
+    objs = []
+    for o in src["objects"]:
+        objs.append(o)
+        objs.append({**o, "material": red})
+    src["objects"] = objs
+    scene = rt.SceneBuilder.from_json(json.dumps(src)).finalize(SEED)
+    gpu.upload(scene, bvh)
+    # the query agrees ray by ray, object index included (the tied pair differ only in material)
+    rng = np.random.default_rng(3)
+    rays = np.hstack([np.array([13.0, 2.0, 3.0]) + rng.normal(scale=0.2, size=(512, 3)),
+                      rng.uniform([-13.0, -2.5, -3.5], [-9.0, -1.5, 1.5], size=(512, 3))])
+    osc = O.OracleScene(scene)
+    ref = [osc.hit(r) for r in rays]
+    for traversal in ("render", "binary"):
+        bad = [(i, g.object, h.object, h.t) for i, (g, h) in enumerate(zip(gpu.hit(rays, 0.001, float("inf"),
+                                                                               traversal=traversal), ref))
+               if g.object != (h.object if h.hit else -1)]
+        _log(f"ties:duplicated_random_scene_rays:{bvh}:{traversal}", bad=len(bad), first=bad[:8],
+             rays=rays[[b[0] for b in bad[:8]]].tolist())
+        assert not bad, (traversal, len(bad), bad[:4])
+    assert sum(h.hit for h in ref) > 100
+    cam = rt.default_camera(48, "std16x9")
+    spp = 4
+    for depth in (1, 2, 3):  # (diagnostic: the bounce at which a departure starts)
+        i_d = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=depth, seed=SEED, sample_chunk=spp))
+        o_d, _ = O.OracleScene(scene).render(cam, O.params(spp, depth, SEED))
+        _log(f"ties:duplicated_random_scene_depth:{bvh}:{depth}",
+             departure_px=float(np.any(np.abs(i_d - o_d) > 1e-10 * spp, axis=-1).mean()))
+    img = gpu.render(cam, rt.RenderSettings(samples=spp, max_reflect=50, seed=SEED, sample_chunk=spp))
+    ora, _ = O.OracleScene(scene).render(cam, O.params(spp, 50, SEED))
+    dep = float(np.any(np.abs(img - ora) > 1e-10 * spp, axis=-1).mean())
+    _log(f"ties:duplicated_random_scene:{bvh}", departure_px=dep, exact=float(np.mean(img == ora)))
+    check_parity(img, ora, spp)
