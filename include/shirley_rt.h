@@ -55,7 +55,8 @@ enum { RT_SKY_ABOVE = 0, RT_SKY_FLAT = 1, RT_SKY_NONE = 2 };
 /* BVH builder selection for rt_scene_upload */
 enum {
   RT_BVH_REFERENCE = 0, /* bvh/bbox_tree/constructor.rs split rules (median/midpoint on min-x/y/z, volume score) */
-  RT_BVH_SAH = 1,       /* surface-area heuristic, exact sweep over every object boundary (performance option; same hits up to measure-zero ties) */
+  RT_BVH_SAH = 1,       /* surface-area heuristic, exact sweep over every object boundary (performance option; the same hits:
+                           exact ties in t go to the reference tree's winner whichever tree is walked) */
   /* node placement flags OR-ed into the builder argument (testing / tuning) */
   RT_BVH_NODES_GLOBAL = 0x100,   /* every node read through L1/L2 (the default) */
   RT_BVH_NODES_HALF_LDS = 0x200, /* top half of the nodes copied into LDS per block (mixed path) */
