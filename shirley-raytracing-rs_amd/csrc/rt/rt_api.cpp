@@ -596,13 +596,12 @@ void set_child_box(DNode4F& n, int slot, const Box* b, double delta) {
 // F(n) = area(n) + G(n, 4)), more slots may open n into its two children, G(n, k) = min over the
 // split j of H(lhs, j) + H(rhs, k - j).  Leaf costs do not depend on the collapse (every object is
 // one child slot) and are left out.
-// w: a node's weight in place of its area (visit_weights), or null.
 struct Collapse4 {
   const BuiltTree* t = nullptr;
   std::vector<double> H, G;    // [n * 5 + j], j = 1..4
   std::vector<int8_t> split;   // argmin j of G(n, k), [n * 5 + k]
   bool ready() const { return t != nullptr; }
-  void build(const BuiltTree& tree, const std::vector<double>* w = nullptr) {
+  void build(const BuiltTree& tree) {
     t = &tree;
     const size_t nn = tree.nodes.size();
     H.assign(nn * 5, 0.0);
@@ -626,7 +625,7 @@ struct Collapse4 {
           const double c = H[b.lhs * 5 + j] + H[b.rhs * 5 + (k - j)];
           if (c < G[n * 5 + k]) { G[n * 5 + k] = c; split[n * 5 + k] = (int8_t)j; }
         }
-      const double f = (w ? (*w)[n] : half_area(b.box)) + G[n * 5 + 4];
+      const double f = half_area(b.box) + G[n * 5 + 4];
       H[n * 5 + 1] = f;
       for (int j = 2; j <= 4; ++j) H[n * 5 + j] = std::min(f, G[n * 5 + j]);
     }
@@ -648,164 +647,13 @@ struct Collapse4 {
   }
 };
 
-// Occlusion-aware node weights for the collapse (SHIRLEY_COLLAPSE=vis; tuning): the area model counts a
-// node for every ray that crosses its box, but an ordered traversal that culls against the closest hit
-// visits a node only if the ray reaches its box before that hit.  So sample the rays a path tracer mostly
-// traces — from points on the objects' surfaces (area-weighted), in the Lambertian direction normal + a
-// random unit vector (lambertian.rs:19-29) — find each one's closest hit on the host (exact for spheres,
-// rects and RectBoxes, an extended object by its box), and weight node n by the number of rays whose
-// segment [0.001, t_hit] enters its box, plus 1 % of the rays times its share of the root's area (an
-// unvisited node still costs by area).  Host-side and scene-only: the collapse changes no hit.
-namespace vis {
-struct Rng {
-  uint64_t s;
-  double u() {  // splitmix64 -> [0, 1)
-    uint64_t z = (s += 0x9e3779b97f4a7c15ull);
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return (double)((z ^ (z >> 31)) >> 11) * 0x1p-53;
-  }
-};
-bool slab(const Box& b, const double o[3], const double inv[3], double t0, double t1, double& te, double& tx) {
-  for (int k = 0; k < 3; ++k) {
-    double a = (b.mn[k] - o[k]) * inv[k], c = (b.mx[k] - o[k]) * inv[k];
-    if (inv[k] < 0.0) std::swap(a, c);
-    t0 = std::max(t0, a);
-    t1 = std::min(t1, c);
-  }
-  te = t0;
-  tx = t1;
-  return t1 > t0;
-}
-// closest t of object o along (org, dir) in (t_min, t_max), or +inf
-double hit_t(const rt_object& o, const double org[3], const double dir[3], const double inv[3], double t_min,
-             double t_max) {
-  const double inf = std::numeric_limits<double>::infinity();
-  if (!is_extended(o) && o.geometry == RT_GEOM_SPHERE) {
-    double oc[3], a = 0, hb = 0, c = 0;
-    for (int k = 0; k < 3; ++k) {
-      oc[k] = org[k] - o.p[k];
-      a += dir[k] * dir[k];
-      hb += oc[k] * dir[k];
-      c += oc[k] * oc[k];
-    }
-    c -= o.p[3] * o.p[3];
-    const double disc = hb * hb - a * c;
-    if (disc < 0.0) return inf;
-    const double sq = std::sqrt(disc);
-    double r = (-hb - sq) / a;
-    if (r < t_min || r > t_max) r = (-hb + sq) / a;
-    return (r < t_min || r > t_max) ? inf : r;
-  }
-  if (!is_extended(o) && o.geometry != RT_GEOM_RECT_BOX) {  // rects: d1, d2 axes and the normal axis
-    const int a1 = o.geometry == RT_GEOM_RECT_YZ ? 1 : 0, a2 = o.geometry == RT_GEOM_RECT_XY ? 1 : 2;
-    const int n = 3 - a1 - a2;
-    const double t = (o.p[4] - org[n]) / dir[n];
-    if (!(t >= t_min && t <= t_max)) return inf;
-    const double x = org[a1] + t * dir[a1], y = org[a2] + t * dir[a2];
-    return (x < o.p[0] || x > o.p[1] || y < o.p[2] || y > o.p[3]) ? inf : t;
-  }
-  double te, tx;  // a RectBox (its faces: the box's entry, or its exit from inside), an extended object's box
-  if (!slab(object_box(o), org, inv, t_min, t_max, te, tx)) return inf;
-  return te > t_min ? te : tx;
-}
-}  // namespace vis
-
-std::vector<double> visit_weights(const BuiltTree& t, const rt_scene_desc* d, int n_rays) {
-  std::vector<double> w(t.nodes.size(), 0.0);
-  if (t.root < 0 || d->n_objects <= 0) return w;
-  // surface-area CDF over the objects (extended ones by their box)
-  std::vector<double> cdf((size_t)d->n_objects);
-  double acc = 0.0;
-  for (int i = 0; i < d->n_objects; ++i) {
-    const rt_object& o = d->objects[i];
-    double a;
-    if (!is_extended(o) && o.geometry == RT_GEOM_SPHERE) a = 4.0 * M_PI * o.p[3] * o.p[3];
-    else if (!is_extended(o) && o.geometry != RT_GEOM_RECT_BOX) a = (o.p[1] - o.p[0]) * (o.p[3] - o.p[2]);
-    else a = 2.0 * half_area(object_box(o));
-    acc += std::isfinite(a) && a > 0.0 ? a : 0.0;
-    cdf[i] = acc;
-  }
-  if (!(acc > 0.0)) return w;
-  vis::Rng rng{0x5eedc011a95e4ull};
-  std::vector<int32_t> stk;
-  for (int r = 0; r < n_rays; ++r) {
-    const int i = (int)(std::lower_bound(cdf.begin(), cdf.end(), rng.u() * acc) - cdf.begin());
-    const rt_object& o = d->objects[std::min(i, d->n_objects - 1)];
-    double p[3], nrm[3] = {0, 0, 0};
-    if (!is_extended(o) && o.geometry == RT_GEOM_SPHERE) {
-      const double z = 2.0 * rng.u() - 1.0, ph = 2.0 * M_PI * rng.u(), s = std::sqrt(std::max(0.0, 1.0 - z * z));
-      nrm[0] = s * std::cos(ph); nrm[1] = s * std::sin(ph); nrm[2] = z;
-      for (int k = 0; k < 3; ++k) p[k] = o.p[k] + std::fabs(o.p[3]) * nrm[k];
-    } else if (!is_extended(o) && o.geometry != RT_GEOM_RECT_BOX) {
-      const int a1 = o.geometry == RT_GEOM_RECT_YZ ? 1 : 0, a2 = o.geometry == RT_GEOM_RECT_XY ? 1 : 2;
-      const int n = 3 - a1 - a2;
-      p[a1] = o.p[0] + (o.p[1] - o.p[0]) * rng.u();
-      p[a2] = o.p[2] + (o.p[3] - o.p[2]) * rng.u();
-      p[n] = o.p[4];
-      nrm[n] = rng.u() < 0.5 ? 1.0 : -1.0;
-    } else {  // a face of the box, by area
-      const Box b = object_box(o);
-      const double e[3] = {b.mx[0] - b.mn[0], b.mx[1] - b.mn[1], b.mx[2] - b.mn[2]};
-      const double fa[3] = {e[1] * e[2], e[0] * e[2], e[0] * e[1]};
-      double x = rng.u() * (fa[0] + fa[1] + fa[2]);
-      const int n = x < fa[0] ? 0 : (x < fa[0] + fa[1] ? 1 : 2);
-      const bool hi = rng.u() < 0.5;
-      for (int k = 0; k < 3; ++k) p[k] = k == n ? (hi ? b.mx[k] : b.mn[k]) : b.mn[k] + e[k] * rng.u();
-      nrm[n] = hi ? 1.0 : -1.0;
-    }
-    double dir[3], inv[3], l2;
-    do {  // normal + a random unit vector (rejection in the unit ball, normalised)
-      double v[3];
-      for (int k = 0; k < 3; ++k) v[k] = 2.0 * rng.u() - 1.0;
-      l2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
-      if (!(l2 <= 1.0 && l2 > 1e-12)) { l2 = 0.0; continue; }
-      const double s = 1.0 / std::sqrt(l2);
-      for (int k = 0; k < 3; ++k) dir[k] = nrm[k] + v[k] * s;
-      l2 = dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2];
-    } while (!(l2 > 1e-12));
-    for (int k = 0; k < 3; ++k) inv[k] = 1.0 / dir[k];
-    // closest hit (a plain stack walk; order does not matter for the result)
-    double th = std::numeric_limits<double>::infinity(), te, tx;
-    stk.assign(1, t.root);
-    while (!stk.empty()) {
-      const BuildNode& b = t.nodes[stk.back()];
-      stk.pop_back();
-      if (!vis::slab(b.box, p, inv, 0.001, th, te, tx)) continue;
-      if (b.leaf >= 0) {
-        th = std::min(th, vis::hit_t(d->objects[b.leaf], p, dir, inv, 0.001, th));
-        continue;
-      }
-      stk.push_back(b.lhs);
-      stk.push_back(b.rhs);
-    }
-    // the nodes a culling traversal must visit: the segment [0.001, th] enters their box
-    stk.assign(1, t.root);
-    while (!stk.empty()) {
-      const int32_t n = stk.back();
-      stk.pop_back();
-      const BuildNode& b = t.nodes[n];
-      if (!vis::slab(b.box, p, inv, 0.001, th, te, tx)) continue;
-      w[n] += 1.0;
-      if (b.leaf < 0) {
-        stk.push_back(b.lhs);
-        stk.push_back(b.rhs);
-      }
-    }
-  }
-  const double ra = half_area(t.nodes[t.root].box);
-  for (size_t n = 0; n < w.size(); ++n)
-    w[n] += 0.01 * n_rays * (ra > 0.0 ? half_area(t.nodes[n].box) / ra : 0.0);
-  return w;
-}
-
 // use_dp: the optimal collapse (Collapse4) instead of the greedy one (open the largest-area internal
 // child until four slots are filled).  rt_scene_upload picks it for the scenes the megakernel runs with
 // the whole scene in LDS, greedy for the rest.
 void flatten4(const BuiltTree& t, const rt_scene_desc* d, double delta, std::vector<DNode4F>& out,
-              int32_t& stack_bound, bool use_dp, const std::vector<double>* weights = nullptr) {
+              int32_t& stack_bound, bool use_dp) {
   Collapse4 dp;
-  if (t.root >= 0 && use_dp) dp.build(t, weights);
+  if (t.root >= 0 && use_dp) dp.build(t);
   out.clear();
   DNode4F top{};
   for (int k = 0; k < 4; ++k) {
@@ -1510,16 +1358,13 @@ int rt_scene_upload(rt_ctx* c, const rt_scene_desc* d, int32_t builder) {
              kLdsBytes;
     };
     const char* e = getenv("SHIRLEY_COLLAPSE_DP");
-    const char* cv = getenv("SHIRLEY_COLLAPSE");
-    const bool use_vis = cv && std::strcmp(cv, "vis") == 0;
-    const bool want = use_vis || (e ? atoi(e) != 0
-                        : (exts.empty() && (placement == 0 || placement == RT_BVH_NODES_LDS) && scene_in_lds(nodes4, stack4)));
+    const bool want = e ? atoi(e) != 0
+                        : (exts.empty() && (placement == 0 || placement == RT_BVH_NODES_LDS) && scene_in_lds(nodes4, stack4));
     if (want) {
       std::vector<DNode4F> dp4;
       int32_t dp_stack = 1;
-      const std::vector<double> vw = use_vis ? visit_weights(tree, d, 1 << 14) : std::vector<double>();
-      flatten4(tree, d, infl.delta, dp4, dp_stack, true, use_vis ? &vw : nullptr);
-      if (e || use_vis || scene_in_lds(dp4, dp_stack)) {
+      flatten4(tree, d, infl.delta, dp4, dp_stack, true);
+      if (e || scene_in_lds(dp4, dp_stack)) {
         nodes4.swap(dp4);
         stack4 = dp_stack;
       }
